@@ -1,0 +1,671 @@
+// capi.cpp — the C ABI (include/fnnue.h).  Host runtime: net ownership, device
+// contexts (one per GPU, weights resident in HBM), chunked launches, error
+// mapping to fishnet's PositionFailed semantics, batch building.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/fnnue.h"
+#include "board.h"
+#include "kernels.h"
+#include "net.h"
+
+using namespace fnnue;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(FNNUE_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                    \
+  do {                                         \
+    hipError_t _e = (expr);                    \
+    if (_e != hipSuccess) return hip_fail(_e, what); \
+  } while (0)
+
+// Positions per launch pair; the transformed-feature workspace is
+// kChunk * hd bytes (1 GiB at hd = 1024).
+constexpr uint32_t kChunk = 1u << 20;
+
+}  // namespace
+
+struct fnnue_net {
+  Net net;
+};
+
+struct fnnue_ctx {
+  int device = 0;
+  uint32_t hd = 0;
+  uint8_t* image = nullptr;
+  size_t image_bytes = 0;
+  NetPtrs ptrs{};
+  uint8_t* x = nullptr;        // [kChunk][hd] transformed features
+  uint8_t* bucket = nullptr;   // [kChunk]
+  uint32_t* err = nullptr;     // latched position errors
+  hipStream_t stream = nullptr;
+  // host-API staging
+  fnnue_pos* d_pos = nullptr;
+  uint32_t* d_off = nullptr;
+  int32_t* d_psqt = nullptr;
+  int32_t* d_positional = nullptr;
+  size_t stage_cap = 0, off_cap = 0;
+  bool timing = false;
+  std::vector<std::array<hipEvent_t, 3>> evpool;  // per timed launch: before ft, between, after stack
+  size_t evused = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+void ctx_destroy(fnnue_ctx* c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  for (auto& trio : c->evpool)
+    for (auto e : trio)
+      if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off,
+                  (void*)c->d_psqt, (void*)c->d_positional})
+    if (p) (void)hipFree(p);
+  delete c;
+}
+
+NetPtrs make_ptrs(uint8_t* img, uint32_t hd) {
+  const ImageLayout L = image_layout(hd);
+  NetPtrs p;
+  p.ft_w = reinterpret_cast<const int16_t*>(img + L.ft_w);
+  p.ft_bias = reinterpret_cast<const int16_t*>(img + L.ft_bias);
+  p.psqt_w = reinterpret_cast<const int32_t*>(img + L.psqt_w);
+  p.w0 = reinterpret_cast<const int8_t*>(img + L.w0);
+  p.b0 = reinterpret_cast<const int32_t*>(img + L.b0);
+  p.w1 = reinterpret_cast<const int8_t*>(img + L.w1);
+  p.b1 = reinterpret_cast<const int32_t*>(img + L.b1);
+  p.w2 = reinterpret_cast<const int8_t*>(img + L.w2);
+  p.b2 = reinterpret_cast<const int32_t*>(img + L.b2);
+  return p;
+}
+
+// Allocates everything except the image contents.
+int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) return fail(FNNUE_E_DEVICE, "no HIP device available");
+  if (device < 0 || device >= ndev) return fail(FNNUE_E_DEVICE, "device ordinal out of range");
+  if (!kernels_support_hd(hd)) return fail(FNNUE_E_ARCH, "no kernel instantiation for hd " + std::to_string(hd));
+  std::unique_ptr<fnnue_ctx, void (*)(fnnue_ctx*)> c(new (std::nothrow) fnnue_ctx, ctx_destroy);
+  if (!c) return fail(FNNUE_E_OOM, "host allocation failed");
+  c->device = device;
+  c->hd = hd;
+  DeviceGuard g(device);
+  c->image_bytes = image_layout(hd).total;
+  if (hipMalloc(&c->image, c->image_bytes) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (net image)");
+  if (hipMalloc(&c->x, (size_t)kChunk * hd) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
+  if (hipMalloc(&c->bucket, kChunk) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
+  if (hipMalloc(&c->err, sizeof(uint32_t)) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (error word)");
+  HIP_TRY(hipMemset(c->err, 0, sizeof(uint32_t)), "hipMemset");
+  HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+  c->ptrs = make_ptrs(c->image, hd);
+  *out = c.release();
+  return FNNUE_OK;
+}
+
+int ensure_stage(fnnue_ctx* c, size_t npos, size_t noff) {
+  if (npos > c->stage_cap) {
+    for (void* p : {(void*)c->d_pos, (void*)c->d_psqt, (void*)c->d_positional})
+      if (p) (void)hipFree(p);
+    c->d_pos = nullptr;
+    c->d_psqt = c->d_positional = nullptr;
+    c->stage_cap = 0;
+    if (hipMalloc(&c->d_pos, npos * sizeof(fnnue_pos)) != hipSuccess ||
+        hipMalloc(&c->d_psqt, npos * sizeof(int32_t)) != hipSuccess ||
+        hipMalloc(&c->d_positional, npos * sizeof(int32_t)) != hipSuccess)
+      return fail(FNNUE_E_OOM, "device allocation (staging)");
+    c->stage_cap = npos;
+  }
+  if (noff > c->off_cap) {
+    if (c->d_off) (void)hipFree(c->d_off);
+    c->d_off = nullptr;
+    c->off_cap = 0;
+    if (hipMalloc(&c->d_off, noff * sizeof(uint32_t)) != hipSuccess)
+      return fail(FNNUE_E_OOM, "device allocation (offsets)");
+    c->off_cap = noff;
+  }
+  return FNNUE_OK;
+}
+
+int latched(fnnue_ctx* c) {
+  uint32_t h = 0;
+  HIP_TRY(hipMemcpy(&h, c->err, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy(error word)");
+  if (h) {
+    HIP_TRY(hipMemset(c->err, 0, sizeof(uint32_t)), "hipMemset");
+    return fail(FNNUE_E_POSITION, "batch contains an invalid position (needs one king per side, <= 32 pieces, "
+                                  "valid piece codes, stm 0/1)");
+  }
+  return FNNUE_OK;
+}
+
+bool valid_host_pos(const fnnue_pos& p) {
+  int n = 0, wk = 0, bk = 0;
+  for (int s = 0; s < 64; ++s) {
+    const int pc = (p.sq[s >> 1] >> (4 * (s & 1))) & 15;
+    if (!pc) continue;
+    if (pc == 7 || pc == 8 || pc == 15) return false;
+    ++n;
+    wk += pc == 6;
+    bk += pc == 14;
+  }
+  return wk == 1 && bk == 1 && n <= 32 && p.stm <= 1;
+}
+
+// Timing events for the next launch (grown on demand, reused after a read).
+int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
+  *out = nullptr;
+  if (!c->timing) return FNNUE_OK;
+  if (c->evused == c->evpool.size()) {
+    std::array<hipEvent_t, 3> trio{nullptr, nullptr, nullptr};
+    for (auto& e : trio) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+    c->evpool.push_back(trio);
+  }
+  *out = &c->evpool[c->evused++];
+  return FNNUE_OK;
+}
+
+// Runs the stack kernel for [0, n) of the workspace and records timing.
+int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 3>* ev) {
+  if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
+  HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, s), "stack kernel launch");
+  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s), "hipEventRecord");
+  return FNNUE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fnnue_last_error(void) { return g_err.c_str(); }
+uint32_t fnnue_abi_version(void) { return (1u << 16) | 0u; }
+
+int fnnue_net_load_mem(const void* buf, size_t len, fnnue_net** out) {
+  if (!buf || !out) return fail(FNNUE_E_ARG, "null argument");
+  *out = nullptr;
+  std::unique_ptr<fnnue_net> n(new (std::nothrow) fnnue_net);
+  if (!n) return fail(FNNUE_E_OOM, "host allocation failed");
+  std::string err;
+  try {
+    const int rc = parse_net(static_cast<const uint8_t*>(buf), len, n->net, err);
+    if (rc) return fail(rc, err);
+  } catch (const std::bad_alloc&) {
+    return fail(FNNUE_E_OOM, "host allocation failed");
+  }
+  *out = n.release();
+  return FNNUE_OK;
+}
+
+int fnnue_net_load(const char* path, fnnue_net** out) {
+  if (!path || !out) return fail(FNNUE_E_ARG, "null argument");
+  *out = nullptr;
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  if (!f) return fail(FNNUE_E_IO, std::string("cannot open ") + path);
+  const std::streamsize len = f.tellg();
+  f.seekg(0);
+  std::vector<uint8_t> buf((size_t)len);
+  if (!f.read(reinterpret_cast<char*>(buf.data()), len)) return fail(FNNUE_E_IO, std::string("cannot read ") + path);
+  return fnnue_net_load_mem(buf.data(), buf.size(), out);
+}
+
+int fnnue_net_info(const fnnue_net* net, uint32_t* hd, uint32_t* file_hash, const char** desc) {
+  if (!net) return fail(FNNUE_E_ARG, "null net");
+  if (hd) *hd = net->net.hd;
+  if (file_hash) *file_hash = net->net.file_hash;
+  if (desc) *desc = net->net.desc.c_str();
+  return FNNUE_OK;
+}
+
+void fnnue_net_free(fnnue_net* net) { delete net; }
+
+int fnnue_net_synthesize(uint64_t seed, uint32_t hd, uint32_t flags, void** buf, size_t* len) {
+  if (!buf || !len) return fail(FNNUE_E_ARG, "null argument");
+  if (!hd_supported(hd)) return fail(FNNUE_E_ARCH, "unsupported hd");
+  try {
+    Net n;
+    synthesize_net(seed, hd, flags, n);
+    std::vector<uint8_t> bytes;
+    write_net(n, flags & FNNUE_SYNTH_LEB128, bytes);
+    void* p = std::malloc(bytes.size());
+    if (!p) return fail(FNNUE_E_OOM, "host allocation failed");
+    std::memcpy(p, bytes.data(), bytes.size());
+    *buf = p;
+    *len = bytes.size();
+  } catch (const std::bad_alloc&) {
+    return fail(FNNUE_E_OOM, "host allocation failed");
+  }
+  return FNNUE_OK;
+}
+
+void fnnue_buffer_free(void* buf) { std::free(buf); }
+
+int fnnue_device_count(int* count) {
+  if (!count) return fail(FNNUE_E_ARG, "null argument");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return FNNUE_OK;
+}
+
+int fnnue_net_image_size(const fnnue_net* net, size_t* bytes) {
+  if (!net || !bytes) return fail(FNNUE_E_ARG, "null argument");
+  *bytes = image_layout(net->net.hd).total;
+  return FNNUE_OK;
+}
+
+int fnnue_net_image_pack(const fnnue_net* net, void* host_buf, size_t bytes) {
+  if (!net || !host_buf) return fail(FNNUE_E_ARG, "null argument");
+  if (bytes < image_layout(net->net.hd).total) return fail(FNNUE_E_CAPACITY, "image buffer too small");
+  pack_image(net->net, static_cast<uint8_t*>(host_buf));
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_create(const fnnue_net* net, int device, fnnue_ctx** out) {
+  if (!net || !out) return fail(FNNUE_E_ARG, "null argument");
+  fnnue_ctx* c = nullptr;
+  int rc = ctx_alloc(device, net->net.hd, &c);
+  if (rc) return rc;
+  std::vector<uint8_t> img;
+  try {
+    img.resize(c->image_bytes);
+  } catch (const std::bad_alloc&) {
+    ctx_destroy(c);
+    return fail(FNNUE_E_OOM, "host allocation failed");
+  }
+  pack_image(net->net, img.data());
+  DeviceGuard g(device);
+  hipError_t e = hipMemcpy(c->image, img.data(), img.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    ctx_destroy(c);
+    return hip_fail(e, "hipMemcpy(net image)");
+  }
+  *out = c;
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_create_from_image(int device, uint32_t hd, const void* device_image, size_t bytes, fnnue_ctx** out) {
+  if (!device_image || !out) return fail(FNNUE_E_ARG, "null argument");
+  if (!hd_supported(hd)) return fail(FNNUE_E_ARCH, "unsupported hd");
+  if (bytes != image_layout(hd).total) return fail(FNNUE_E_ARG, "image size does not match hd");
+  fnnue_ctx* c = nullptr;
+  int rc = ctx_alloc(device, hd, &c);
+  if (rc) return rc;
+  DeviceGuard g(device);
+  hipError_t e = hipMemcpy(c->image, device_image, bytes, hipMemcpyDeviceToDevice);
+  if (e != hipSuccess) {
+    ctx_destroy(c);
+    return hip_fail(e, "hipMemcpy(device image)");
+  }
+  *out = c;
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_image(fnnue_ctx* ctx, const void** device_image, size_t* bytes) {
+  if (!ctx || !device_image || !bytes) return fail(FNNUE_E_ARG, "null argument");
+  *device_image = ctx->image;
+  *bytes = ctx->image_bytes;
+  return FNNUE_OK;
+}
+
+void fnnue_ctx_free(fnnue_ctx* ctx) { ctx_destroy(ctx); }
+
+int fnnue_ctx_set_timing(fnnue_ctx* ctx, int enable) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  ctx->timing = enable != 0;
+  ctx->evused = 0;
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_timing_read(fnnue_ctx* ctx, uint32_t* launches, double* ft_ms, double* stack_ms) {
+  if (!ctx || !launches || !ft_ms || !stack_ms) return fail(FNNUE_E_ARG, "null argument");
+  *launches = 0;
+  *ft_ms = *stack_ms = 0;
+  DeviceGuard g(ctx->device);
+  for (size_t i = 0; i < ctx->evused; ++i) {
+    auto& e = ctx->evpool[i];
+    float a = 0, b = 0;
+    HIP_TRY(hipEventSynchronize(e[2]), "hipEventSynchronize");
+    HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]), "hipEventElapsedTime");
+    HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]), "hipEventElapsedTime");
+    *ft_ms += a;
+    *stack_ms += b;
+  }
+  *launches = (uint32_t)ctx->evused;
+  ctx->evused = 0;
+  return FNNUE_OK;
+}
+
+int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n, int32_t* d_psqt,
+                                int32_t* d_positional, void* stream) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (n == 0) return FNNUE_OK;
+  if (!d_pos || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  for (size_t b = 0; b < n; b += kChunk) {
+    const uint32_t m = (uint32_t)std::min<size_t>(kChunk, n - b);
+    std::array<hipEvent_t, 3>* ev = nullptr;
+    int rc = next_events(ctx, &ev);
+    if (rc) return rc;
+    if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+    HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
+            "ft_scratch launch");
+    rc = run_chunk_tail(ctx, m, d_positional + b, s, ev);
+    if (rc) return rc;
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint32_t* d_off, size_t ngroups,
+                             size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {
+  // d_off is device memory; the chunking needs the group boundaries on the
+  // host, so this entry point copies them once (ngroups+1 words).
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
+  if (ngroups == 0) return FNNUE_OK;
+  if (!d_pos || !d_off || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  std::vector<uint32_t> off(ngroups + 1);
+  HIP_TRY(hipMemcpyAsync(off.data(), d_off, off.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpy");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  if (off[0] != 0 || off[ngroups] != npos) return fail(FNNUE_E_ARG, "group offsets must span [0, npos)");
+  size_t gb = 0;
+  while (gb < ngroups) {
+    size_t ge = gb;
+    while (ge < ngroups && off[ge + 1] - off[gb] <= kChunk) {
+      if (off[ge + 1] < off[ge]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
+      ++ge;
+    }
+    if (ge == gb) return fail(FNNUE_E_ARG, "a group is larger than the device workspace");
+    const uint32_t base = off[gb], m = off[ge] - off[gb];
+    std::array<hipEvent_t, 3>* ev = nullptr;
+    int rc = next_events(ctx, &ev);
+    if (rc) return rc;
+    if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+    HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs, ctx->x,
+                             d_psqt + base, ctx->bucket, ctx->err, s),
+            "ft_groups launch");
+    rc = run_chunk_tail(ctx, m, d_positional + base, s, ev);
+    if (rc) return rc;
+    gb = ge;
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_check(fnnue_ctx* ctx) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  DeviceGuard g(ctx->device);
+  HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return latched(ctx);
+}
+
+int fnnue_eval_positions(fnnue_ctx* ctx, const fnnue_pos* pos, size_t n, int32_t* psqt, int32_t* positional) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (n == 0) return FNNUE_OK;
+  if (!pos || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
+  for (size_t i = 0; i < n; ++i)
+    if (!valid_host_pos(pos[i])) return fail(FNNUE_E_POSITION, "invalid position at index " + std::to_string(i));
+  DeviceGuard g(ctx->device);
+  const size_t step = std::min<size_t>(n, 4 * (size_t)kChunk);
+  int rc = ensure_stage(ctx, step, 0);
+  if (rc) return rc;
+  for (size_t b = 0; b < n; b += step) {
+    const size_t m = std::min(step, n - b);
+    HIP_TRY(hipMemcpyAsync(ctx->d_pos, pos + b, m * sizeof(fnnue_pos), hipMemcpyHostToDevice, ctx->stream), "H2D");
+    rc = fnnue_eval_positions_device(ctx, ctx->d_pos, m, ctx->d_psqt, ctx->d_positional, ctx->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(psqt + b, ctx->d_psqt, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    HIP_TRY(hipMemcpyAsync(positional + b, ctx->d_positional, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    rc = latched(ctx);
+    if (rc) return rc;
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_eval_groups(fnnue_ctx* ctx, const fnnue_pos* pos, const uint32_t* off, size_t ngroups, int mode,
+                      int32_t* psqt, int32_t* positional) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
+  if (ngroups == 0) return FNNUE_OK;
+  if (!pos || !off || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
+  if (off[0] != 0) return fail(FNNUE_E_ARG, "off[0] must be 0");
+  for (size_t g = 0; g < ngroups; ++g)
+    if (off[g + 1] < off[g]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
+  const size_t npos = off[ngroups];
+  for (size_t i = 0; i < npos; ++i)
+    if (!valid_host_pos(pos[i])) return fail(FNNUE_E_POSITION, "invalid position at index " + std::to_string(i));
+  DeviceGuard g(ctx->device);
+  int rc = ensure_stage(ctx, std::max<size_t>(npos, 1), ngroups + 1);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->d_pos, pos, npos * sizeof(fnnue_pos), hipMemcpyHostToDevice, ctx->stream), "H2D");
+  HIP_TRY(hipMemcpyAsync(ctx->d_off, off, (ngroups + 1) * 4, hipMemcpyHostToDevice, ctx->stream), "H2D");
+  rc = fnnue_eval_groups_device(ctx, ctx->d_pos, ctx->d_off, ngroups, npos, mode, ctx->d_psqt, ctx->d_positional,
+                                ctx->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(psqt, ctx->d_psqt, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+  HIP_TRY(hipMemcpyAsync(positional, ctx->d_positional, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+  HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+  return latched(ctx);
+}
+
+// ---- batch building ----
+
+int fnnue_pos_from_fen(const char* fen, fnnue_pos* out) {
+  if (!fen || !out) return fail(FNNUE_E_ARG, "null argument");
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  *out = b.pack();
+  return FNNUE_OK;
+}
+
+namespace {
+int split_moves(const char* moves, std::vector<std::string>& out) {
+  out.clear();
+  if (!moves) return FNNUE_OK;
+  const char* p = moves;
+  while (*p) {
+    while (*p == ' ' || *p == '\t' || *p == '\n') ++p;
+    const char* q = p;
+    while (*q && *q != ' ' && *q != '\t' && *q != '\n') ++q;
+    if (q > p) out.emplace_back(p, q);
+    p = q;
+  }
+  return FNNUE_OK;
+}
+}  // namespace
+
+int fnnue_game_positions(const char* fen, const char* moves, fnnue_pos* out, size_t cap, size_t* n_out) {
+  if (!fen || !n_out) return fail(FNNUE_E_ARG, "null argument");
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  std::vector<std::string> ms;
+  split_moves(moves, ms);
+  *n_out = ms.size() + 1;
+  if (!out || cap < ms.size() + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  out[0] = b.pack();
+  for (size_t i = 0; i < ms.size(); ++i) {
+    Move m;
+    if (!parse_uci(b, ms[i].c_str(), m))
+      return fail(FNNUE_E_MOVE, "illegal move " + ms[i] + " at ply " + std::to_string(i + 1) + " in " + b.fen());
+    b.do_move(m);
+    out[i + 1] = b.pack();
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_game_children(const char* fen, const char* moves, fnnue_pos* out, size_t cap, uint32_t* off,
+                        size_t off_cap, size_t* n_out, size_t* n_groups) {
+  if (!fen || !n_out || !n_groups) return fail(FNNUE_E_ARG, "null argument");
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  std::vector<std::string> ms;
+  split_moves(moves, ms);
+  std::vector<fnnue_pos> res;
+  std::vector<uint32_t> offs{0};
+  std::vector<Move> legal;
+  for (size_t i = 0; i <= ms.size(); ++i) {
+    res.push_back(b.pack());
+    b.legal_moves(legal);
+    for (const Move& m : legal) {
+      Board c = b;
+      c.do_move(m);
+      res.push_back(c.pack());
+    }
+    offs.push_back((uint32_t)res.size());
+    if (i == ms.size()) break;
+    Move m;
+    if (!parse_uci(b, ms[i].c_str(), m))
+      return fail(FNNUE_E_MOVE, "illegal move " + ms[i] + " at ply " + std::to_string(i + 1));
+    b.do_move(m);
+  }
+  *n_out = res.size();
+  *n_groups = offs.size() - 1;
+  if (!out || !off || cap < res.size() || off_cap < offs.size()) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  std::memcpy(out, res.data(), res.size() * sizeof(fnnue_pos));
+  std::memcpy(off, offs.data(), offs.size() * sizeof(uint32_t));
+  return FNNUE_OK;
+}
+
+int fnnue_random_playouts(uint64_t seed, size_t count, uint32_t min_plies, uint32_t max_plies, int mode, int threads,
+                          fnnue_pos* out, size_t cap, uint32_t* off, size_t off_cap, size_t* n_out,
+                          size_t* n_groups) {
+  if (!n_out || !n_groups || !out) return fail(FNNUE_E_ARG, "null argument");
+  if (mode < FNNUE_PLAYOUT_FINAL || mode > FNNUE_PLAYOUT_CHILDREN) return fail(FNNUE_E_ARG, "bad playout mode");
+  if (min_plies > max_plies) return fail(FNNUE_E_ARG, "min_plies > max_plies");
+  if (mode != FNNUE_PLAYOUT_FINAL && !off) return fail(FNNUE_E_ARG, "grouped modes need off[]");
+  Board start;
+  board_from_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1", start, nullptr);
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  // Each playout is generated independently from (seed, index), so results do
+  // not depend on the thread count.  Per-playout outputs are gathered into
+  // per-thread vectors and concatenated in index order.
+  struct Part {
+    std::vector<fnnue_pos> pos;
+    std::vector<uint32_t> sizes;  // group sizes
+  };
+  std::vector<Part> parts(threads);
+  auto work = [&](int t) {
+    const size_t b = count * t / threads, e = count * (t + 1) / threads;
+    Part& P = parts[t];
+    for (size_t i = b; i < e; ++i) {
+      uint64_t st = seed ^ (0xD1B54A32D192ED03ull * (i + 1));
+      const uint32_t L = min_plies + (uint32_t)(splitmix64(st) % (uint64_t)(max_plies - min_plies + 1));
+      Board bd = start;
+      auto emit = [&](const Board& x) {
+        if (mode == FNNUE_PLAYOUT_PLIES) {
+          P.pos.push_back(x.pack());
+        } else if (mode == FNNUE_PLAYOUT_CHILDREN) {
+          P.pos.push_back(x.pack());
+          std::vector<Move> ch;
+          x.legal_moves(ch);
+          for (const Move& m : ch) {
+            Board c = x;
+            c.do_move(m);
+            P.pos.push_back(c.pack());
+          }
+          P.sizes.push_back((uint32_t)(ch.size() + 1));
+        }
+      };
+      const size_t before = P.pos.size();
+      emit(bd);
+      for (uint32_t ply = 0; ply < L; ++ply) {
+        Move m;
+        if (bd.halfmove >= 100 || !bd.random_legal_move(st, m)) break;
+        bd.do_move(m);
+        emit(bd);
+      }
+      if (mode == FNNUE_PLAYOUT_FINAL) P.pos.push_back(bd.pack());
+      else if (mode == FNNUE_PLAYOUT_PLIES) P.sizes.push_back((uint32_t)(P.pos.size() - before));
+    }
+  };
+  try {
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  } catch (const std::exception& ex) {
+    return fail(FNNUE_E_OOM, std::string("playout generation failed: ") + ex.what());
+  }
+  size_t total = 0, groups = 0;
+  for (auto& P : parts) {
+    total += P.pos.size();
+    groups += P.sizes.size();
+  }
+  *n_out = total;
+  *n_groups = groups;
+  if (cap < total) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  if (mode != FNNUE_PLAYOUT_FINAL && off_cap < groups + 1) return fail(FNNUE_E_CAPACITY, "offset buffer too small");
+  size_t k = 0, gk = 0;
+  if (mode != FNNUE_PLAYOUT_FINAL) off[0] = 0;
+  for (auto& P : parts) {
+    std::memcpy(out + k, P.pos.data(), P.pos.size() * sizeof(fnnue_pos));
+    for (uint32_t sz : P.sizes) {
+      off[gk + 1] = off[gk] + sz;
+      ++gk;
+    }
+    k += P.pos.size();
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_perft(const char* fen, int depth, uint64_t* nodes) {
+  if (!fen || !nodes || depth < 0) return fail(FNNUE_E_ARG, "bad argument");
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  *nodes = perft(b, depth);
+  return FNNUE_OK;
+}
+
+int fnnue_selftest_mfma(int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(FNNUE_E_DEVICE, "no such device");
+  DeviceGuard g(device);
+  int bad = -1;
+  HIP_TRY(run_mfma_selftest(&bad), "mfma selftest");
+  if (bad) return fail(FNNUE_E_DEVICE, "MFMA operand layout mismatch: " + std::to_string(bad) + " outputs differ");
+  return FNNUE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,551 @@
+// kernels.hip — CDNA4 (gfx950) kernels for batched Stockfish NNUE evaluation.
+//
+// Hot path (SURVEY.md §8a rows a2–a8):
+//   ft_scratch  HalfKAv2_hm feature indices + FeatureTransformer refresh +
+//               transform (clamp, pairwise product) + PSQT term.  One 64-lane
+//               wave per position; the wave owns both int16 accumulators in
+//               VGPRs: lane l holds elements [l*EPL, l*EPL+EPL) of each half,
+//               so every weight-row read is a 1 KiB-contiguous wave load
+//               (HD=1024: global_load_dwordx4 per lane) and the pairwise
+//               product (j, j+HD/2) never crosses lanes.
+//   ft_groups   Same, but walking a group of positions (a game's plies, or a
+//               parent and its children) with incremental add/sub of the
+//               changed feature rows; refresh when the perspective's king moves.
+//   stack       fc_0 (HD -> 16) and fc_1 (30 -> 32) as int8 MFMA
+//               (v_mfma_i32_16x16x64_i8) over 16-position tiles, SqrCReLU /
+//               CReLU / fc_2 / fwd term in VALU.
+// Upstream formulas restated in oracle/nnue_oracle.c (test-only); constants in
+// net.h.  All arithmetic is integer and order-independent, so results are
+// bit-exact regardless of scheduling.
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+#include "net.h"
+
+namespace fnnue {
+
+namespace {
+
+constexpr int kZeroRow = kFeatures;  // all-zero padding row in ft_w / psqt_w
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+template <int N> struct Vec {
+  typedef unsigned short u16 __attribute__((ext_vector_type(N)));
+  typedef short s16 __attribute__((ext_vector_type(N)));
+  typedef unsigned char u8 __attribute__((ext_vector_type(N)));
+};
+
+// HalfKAv2_hm::make_index (upstream features/half_ka_v2_hm.cpp):
+//   orient(p, s, ksq) = s ^ (p * SQ_A8) ^ ((file_of(ksq) < FILE_E) * SQ_H1)
+//   index = orient(s) + PieceSquareIndex[p][pc] + PS_NB * KingBuckets[orient(ksq)]
+// KingBuckets[o] = 4*(7-rank(o)) + (7-file(o)) for the e..h files o lands on.
+__device__ __forceinline__ int make_index(int persp, int s, int pc, int ksq) {
+  const int flip = (persp ? 56 : 0) ^ (((ksq & 7) < 4) ? 7 : 0);
+  const int os = s ^ flip, ok = ksq ^ flip;
+  const int type = pc & 7;
+  const int plane = type == 6 ? 10 : 2 * (type - 1) + ((pc >> 3) != persp);
+  return os + 64 * plane + 704 * (4 * (7 - (ok >> 3)) + (7 - (ok & 7)));
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Decoded position as seen by one wave: lane l = square l.
+struct Decoded {
+  int pc;        // piece on this lane's square
+  uint64_t occ;  // occupied squares
+  int stm, wk, bk, cnt;
+  bool ok;
+};
+
+__device__ __forceinline__ Decoded decode(const fnnue_pos* p, int lane) {
+  Decoded d;
+  const uint8_t* pp = reinterpret_cast<const uint8_t*>(p);
+  const int byte = pp[lane >> 1];
+  d.pc = (byte >> ((lane & 1) * 4)) & 15;
+  d.stm = pp[32];
+  d.occ = __ballot(d.pc != 0);
+  const uint64_t wkm = __ballot(d.pc == 6), bkm = __ballot(d.pc == 14);
+  const uint64_t bad = __ballot(d.pc == 7 || d.pc == 8 || d.pc == 15);
+  d.cnt = __popcll(d.occ);
+  d.ok = !bad && __popcll(wkm) == 1 && __popcll(bkm) == 1 && d.cnt <= 32 && d.stm <= 1;
+  d.wk = wkm ? __builtin_ctzll(wkm) : 0;
+  d.bk = bkm ? __builtin_ctzll(bkm) : 0;
+  return d;
+}
+
+// FeatureTransformer::transform for one perspective half (upstream
+// nnue_feature_transformer.h): out[j] = clamp(a[j],0,127) * clamp(a[j+HD/2],0,127) / 128.
+template <int EPL>
+__device__ __forceinline__ void transform_store(typename Vec<EPL>::u16 lo, typename Vec<EPL>::u16 hi, uint8_t* dst) {
+  typedef typename Vec<EPL>::s16 s16;
+  typedef typename Vec<EPL>::u16 u16;
+  const s16 zero = (s16)0, top = (s16)127;
+  s16 a = __builtin_elementwise_min(__builtin_elementwise_max((s16)lo, zero), top);
+  s16 b = __builtin_elementwise_min(__builtin_elementwise_max((s16)hi, zero), top);
+  u16 prod = ((u16)a * (u16)b) >> (u16)7;
+  *reinterpret_cast<typename Vec<EPL>::u8*>(dst) = __builtin_convertvector(prod, typename Vec<EPL>::u8);
+}
+
+// Adds (SIGN=+1) or subtracts the weight rows f(s) for every square s in `mask`
+// to the lane's accumulator slice.  f is a per-lane value read with readlane,
+// so each row address is wave-uniform (scalar base + lane offset) and each row
+// is two 1 KiB-contiguous wave loads (HD=1024).  U rows are in flight per step.
+template <int HD, int U>
+__device__ __forceinline__ void add_rows(const int16_t* __restrict__ ftw, uint64_t mask, int f_add, int f_sub,
+                                         bool do_sub, typename Vec<HD / 128>::u16& lo,
+                                         typename Vec<HD / 128>::u16& hi, int lane) {
+  constexpr int EPL = HD / 128;
+  typedef typename Vec<EPL>::u16 u16;
+  while (mask) {
+    int fa[U], fs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (mask) {
+        const int s = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        fa[u] = __builtin_amdgcn_readlane(f_add, s);
+        fs[u] = do_sub ? __builtin_amdgcn_readlane(f_sub, s) : kZeroRow;
+      } else {
+        fa[u] = kZeroRow;
+        fs[u] = kZeroRow;
+      }
+    }
+    u16 va[U][2], vs[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const u16* ra = reinterpret_cast<const u16*>(ftw + (size_t)fa[u] * HD);
+      va[u][0] = ra[lane];
+      va[u][1] = ra[64 + lane];
+      if (do_sub) {
+        const u16* rs = reinterpret_cast<const u16*>(ftw + (size_t)fs[u] * HD);
+        vs[u][0] = rs[lane];
+        vs[u][1] = rs[64 + lane];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      lo += va[u][0];
+      hi += va[u][1];
+      if (do_sub) {
+        lo -= vs[u][0];
+        hi -= vs[u][1];
+      }
+    }
+  }
+}
+
+// PSQT term: (psqtAcc[stm][b] - psqtAcc[~stm][b]) / 2 with C truncation.
+__device__ __forceinline__ int psqt_term(const int32_t* __restrict__ psqw, const Decoded& d, int lane, int bucket) {
+  int fw = kZeroRow, fb = kZeroRow;
+  if (d.pc) {
+    fw = make_index(0, lane, d.pc, d.wk);
+    fb = make_index(1, lane, d.pc, d.bk);
+  }
+  const int v = psqw[fw * kPsqtBuckets + bucket] - psqw[fb * kPsqtBuckets + bucket];
+  int tot = wave_sum(v);
+  if (d.stm) tot = -tot;
+  return tot / 2;
+}
+
+template <int HD>
+__device__ __forceinline__ void store_invalid(uint8_t* x, int lane) {
+  constexpr int EPL = HD / 128;
+  const typename Vec<EPL>::u8 z = (typename Vec<EPL>::u8)0;
+  *reinterpret_cast<typename Vec<EPL>::u8*>(x + lane * EPL) = z;
+  *reinterpret_cast<typename Vec<EPL>::u8*>(x + HD / 2 + lane * EPL) = z;
+}
+
+// ---------------------------------------------------------------------------
+// ft_scratch: accumulators from scratch (upstream update_accumulator refresh).
+template <int HD, int U>
+__global__ __launch_bounds__(256) void ft_scratch_kernel(const fnnue_pos* __restrict__ pos, uint32_t n, NetPtrs net,
+                                                         uint8_t* __restrict__ x, int32_t* __restrict__ psqt,
+                                                         uint8_t* __restrict__ bucket_out, uint32_t* __restrict__ err) {
+  constexpr int EPL = HD / 128;
+  typedef typename Vec<EPL>::u16 u16;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const u16* bias = reinterpret_cast<const u16*>(net.ft_bias);
+  const u16 b_lo = bias[lane], b_hi = bias[64 + lane];
+  for (uint32_t p = wid; p < n; p += nw) {
+    const Decoded d = decode(pos + p, lane);
+    uint8_t* xo = x + (size_t)p * HD;
+    if (!d.ok) {
+      store_invalid<HD>(xo, lane);
+      if (lane == 0) {
+        atomicOr(err, 1u);
+        psqt[p] = 0;
+        bucket_out[p] = 0xFF;
+      }
+      continue;
+    }
+    const int bucket = (d.cnt - 1) >> 2;
+    int fw = kZeroRow, fb = kZeroRow;
+    if (d.pc) {
+      fw = make_index(0, lane, d.pc, d.wk);
+      fb = make_index(1, lane, d.pc, d.bk);
+    }
+    const int v = net.psqt_w[fw * kPsqtBuckets + bucket] - net.psqt_w[fb * kPsqtBuckets + bucket];
+    int tot = wave_sum(v);
+    if (d.stm) tot = -tot;
+    u16 w_lo = b_lo, w_hi = b_hi, k_lo = b_lo, k_hi = b_hi;
+    // Both perspectives share the occupancy mask: interleave them so 4U row
+    // halves are in flight per lane.
+    uint64_t mask = d.occ;
+    while (mask) {
+      int f0[U], f1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (mask) {
+          const int s = __builtin_ctzll(mask);
+          mask &= mask - 1;
+          f0[u] = __builtin_amdgcn_readlane(fw, s);
+          f1[u] = __builtin_amdgcn_readlane(fb, s);
+        } else {
+          f0[u] = kZeroRow;
+          f1[u] = kZeroRow;
+        }
+      }
+      u16 r0[U][2], r1[U][2];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u16* a = reinterpret_cast<const u16*>(net.ft_w + (size_t)f0[u] * HD);
+        const u16* b = reinterpret_cast<const u16*>(net.ft_w + (size_t)f1[u] * HD);
+        r0[u][0] = a[lane];
+        r0[u][1] = a[64 + lane];
+        r1[u][0] = b[lane];
+        r1[u][1] = b[64 + lane];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        w_lo += r0[u][0];
+        w_hi += r0[u][1];
+        k_lo += r1[u][0];
+        k_hi += r1[u][1];
+      }
+    }
+    if (d.stm) {
+      transform_store<EPL>(k_lo, k_hi, xo + lane * EPL);
+      transform_store<EPL>(w_lo, w_hi, xo + HD / 2 + lane * EPL);
+    } else {
+      transform_store<EPL>(w_lo, w_hi, xo + lane * EPL);
+      transform_store<EPL>(k_lo, k_hi, xo + HD / 2 + lane * EPL);
+    }
+    if (lane == 0) {
+      psqt[p] = tot / 2;
+      bucket_out[p] = (uint8_t)bucket;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ft_groups: one wave walks a group.  CHAIN: base = previous position of the
+// group; STAR: base = the group's first position (the parent).  Perspective c
+// refreshes when there is no valid base, when its own king moved (upstream
+// HalfKAv2_hm::requires_refresh), or when the delta is larger than a refresh.
+template <int HD, int U>
+__global__ __launch_bounds__(256) void ft_groups_kernel(const fnnue_pos* __restrict__ pos,
+                                                        const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                        uint32_t base_index, int star, NetPtrs net,
+                                                        uint8_t* __restrict__ x, int32_t* __restrict__ psqt,
+                                                        uint8_t* __restrict__ bucket_out,
+                                                        uint32_t* __restrict__ err) {
+  constexpr int EPL = HD / 128;
+  typedef typename Vec<EPL>::u16 u16;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const u16* bias = reinterpret_cast<const u16*>(net.ft_bias);
+  const u16 b_lo = bias[lane], b_hi = bias[64 + lane];
+  for (uint32_t g = wid; g < ngroups; g += nw) {
+    const uint32_t begin = off[g], end = off[g + 1];
+    // Base state (previous ply for CHAIN, parent for STAR).
+    bool have = false;
+    int base_pc = 0, base_wk = 0, base_bk = 0;
+    u16 bw_lo = b_lo, bw_hi = b_hi, bb_lo = b_lo, bb_hi = b_hi;
+    for (uint32_t i = begin; i < end; ++i) {
+      const Decoded d = decode(pos + i, lane);
+      const uint32_t o = i - base_index;
+      uint8_t* xo = x + (size_t)o * HD;
+      if (!d.ok) {
+        store_invalid<HD>(xo, lane);
+        if (lane == 0) {
+          atomicOr(err, 1u);
+          psqt[o] = 0;
+          bucket_out[o] = 0xFF;
+        }
+        if (!star || i == begin) have = false;
+        continue;
+      }
+      const int bucket = (d.cnt - 1) >> 2;
+      const int tot = psqt_term(net.psqt_w, d, lane, bucket);
+      const uint64_t changed = __ballot(d.pc != base_pc);
+      const int nchg = __popcll(changed);
+      u16 w_lo, w_hi, k_lo, k_hi;
+      // White perspective.
+      {
+        const int f_new = d.pc ? make_index(0, lane, d.pc, d.wk) : kZeroRow;
+        if (!have || d.wk != base_wk || 2 * nchg >= d.cnt) {
+          w_lo = b_lo;
+          w_hi = b_hi;
+          add_rows<HD, U>(net.ft_w, d.occ, f_new, kZeroRow, false, w_lo, w_hi, lane);
+        } else {
+          const int f_old = base_pc ? make_index(0, lane, base_pc, d.wk) : kZeroRow;
+          w_lo = bw_lo;
+          w_hi = bw_hi;
+          add_rows<HD, U>(net.ft_w, changed, d.pc != base_pc ? f_new : kZeroRow, f_old, true, w_lo, w_hi, lane);
+        }
+      }
+      // Black perspective.
+      {
+        const int f_new = d.pc ? make_index(1, lane, d.pc, d.bk) : kZeroRow;
+        if (!have || d.bk != base_bk || 2 * nchg >= d.cnt) {
+          k_lo = b_lo;
+          k_hi = b_hi;
+          add_rows<HD, U>(net.ft_w, d.occ, f_new, kZeroRow, false, k_lo, k_hi, lane);
+        } else {
+          const int f_old = base_pc ? make_index(1, lane, base_pc, d.bk) : kZeroRow;
+          k_lo = bb_lo;
+          k_hi = bb_hi;
+          add_rows<HD, U>(net.ft_w, changed, d.pc != base_pc ? f_new : kZeroRow, f_old, true, k_lo, k_hi, lane);
+        }
+      }
+      if (d.stm) {
+        transform_store<EPL>(k_lo, k_hi, xo + lane * EPL);
+        transform_store<EPL>(w_lo, w_hi, xo + HD / 2 + lane * EPL);
+      } else {
+        transform_store<EPL>(w_lo, w_hi, xo + lane * EPL);
+        transform_store<EPL>(k_lo, k_hi, xo + HD / 2 + lane * EPL);
+      }
+      if (lane == 0) {
+        psqt[o] = tot;
+        bucket_out[o] = (uint8_t)bucket;
+      }
+      if (!star || i == begin) {
+        have = true;
+        base_pc = d.pc;
+        base_wk = d.wk;
+        base_bk = d.bk;
+        bw_lo = w_lo;
+        bw_hi = w_hi;
+        bb_lo = k_lo;
+        bb_hi = k_hi;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Layer stacks (upstream nnue_architecture.h Network::propagate).  One wave per
+// tile of 16 positions.  MFMA i32_16x16x64_i8 operand layout (checked on the
+// device by mfma_selftest): lane l holds A[row l&15][k 16(l>>4) .. +15] and
+// B[k 16(l>>4) .. +15][col l&15]; C/D: lane l holds C[row 4(l>>4)+r][col l&15].
+// Transformed features are <= 126 and fc_1 inputs <= 127, so treating the u8
+// activations as signed int8 is exact.
+__device__ __forceinline__ int crelu(int v) { return min(127, max(0, v >> 6)); }
+__device__ __forceinline__ int sqr_crelu(int v) {
+  // min(127, (v*v >> 12) / 128) == min(127, v*v >> 19); clamp |v| first so
+  // the square fits in 32 bits (|v| >= 8160 already saturates).
+  const int a = min(abs(v), 16384);
+  return min(127, (int)(((unsigned)(a * a)) >> 19));
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ bucket,
+                                                    uint32_t n, NetPtrs net, int32_t* __restrict__ positional) {
+  constexpr int KS = HD / 64;
+  __shared__ __attribute__((aligned(16))) uint8_t x1s[4][16][64];
+  __shared__ int32_t fwds[4][16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  // Zero the fc_1 input tile once (k >= 30 stays zero).
+  *reinterpret_cast<v4i*>(&x1s[wv][r16][16 * g]) = (v4i)0;
+  wave_lds_sync();
+  const uint32_t ntiles = (n + 15) / 16;
+  const uint32_t nw = gridDim.x * 4;
+  for (uint32_t tile = blockIdx.x * 4 + wv; tile < ntiles; tile += nw) {
+    const uint32_t p0 = tile * 16;
+    const uint32_t prow = p0 + r16;
+    const bool row_ok = prow < n;
+    const int bk = row_ok ? bucket[prow] : 0xFF;
+    uint32_t bmask = 0;
+#pragma unroll
+    for (int b = 0; b < kStacks; ++b)
+      if (__ballot(bk == b)) bmask |= 1u << b;
+    v4i a[KS];
+    const v4i* xr = reinterpret_cast<const v4i*>(x + (size_t)(row_ok ? prow : p0) * HD);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) a[s] = row_ok ? xr[4 * s + g] : (v4i)0;
+    while (bmask) {
+      const int b = __builtin_ctz(bmask);
+      bmask &= bmask - 1;
+      // fc_0: y[pos][out] = b0 + sum_k x[pos][k] * w0[out][k]
+      v4i acc = (v4i)0;
+      const v4i* wr = reinterpret_cast<const v4i*>(net.w0 + ((size_t)b * kL2 + r16) * HD);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], wr[4 * s + g], acc, 0, 0, 0);
+      const int bias0 = net.b0[b * kL2 + r16];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int y = acc[r] + bias0;
+        const int p = 4 * g + r;
+        if (r16 < kL2 - 1) {
+          x1s[wv][p][r16] = (uint8_t)sqr_crelu(y);
+          x1s[wv][p][15 + r16] = (uint8_t)crelu(y);
+        } else {
+          // fwdOut = y15 * (600 * OutputScale) / (127 * (1 << WeightScaleBits))
+          fwds[wv][p] = (int)(((long long)y * 9600) / 8128);
+        }
+      }
+      wave_lds_sync();
+      // fc_1 (30 -> 32, k padded to 64 with zeros), two MFMAs for outputs 0..15, 16..31.
+      const v4i a1 = g < 2 ? *reinterpret_cast<const v4i*>(&x1s[wv][r16][16 * g]) : (v4i)0;
+      const int8_t* w1b = net.w1 + (size_t)b * kL3 * kFc1In;
+      const v4i wA = g < 2 ? *reinterpret_cast<const v4i*>(w1b + r16 * kFc1In + 16 * g) : (v4i)0;
+      const v4i wB = g < 2 ? *reinterpret_cast<const v4i*>(w1b + (16 + r16) * kFc1In + 16 * g) : (v4i)0;
+      const v4i z0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wA, (v4i)0, 0, 0, 0);
+      const v4i z1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wB, (v4i)0, 0, 0, 0);
+      const int b1a = net.b1[b * kL3 + r16], b1b = net.b1[b * kL3 + 16 + r16];
+      const int w2a = net.w2[b * kL3 + r16], w2b = net.w2[b * kL3 + 16 + r16];
+      int part[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[r] = w2a * crelu(z0[r] + b1a) + w2b * crelu(z1[r] + b1b);
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) part[r] += __shfl_xor(part[r], o);
+      const int b2 = net.b2[b];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 4 * g + r;
+        const int pb = __shfl(bk, p);
+        if (r16 == 0 && pb == b) positional[p0 + p] = b2 + part[r] + fwds[wv][p];
+      }
+      wave_lds_sync();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA layout self test: C = A * B with A[i][k] = (i*7 + k*3) % 19 - 9 and
+// B[k][j] = (k*5 + j*11) % 23 - 11 loaded with the kernels' lane map.
+__global__ void mfma_selftest_kernel(int* out) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, g = lane >> 4;
+  v4i a, b;
+  int8_t* ap = reinterpret_cast<int8_t*>(&a);
+  int8_t* bp = reinterpret_cast<int8_t*>(&b);
+  for (int j = 0; j < 16; ++j) {
+    const int k = 16 * g + j;
+    ap[j] = (int8_t)((r16 * 7 + k * 3) % 19 - 9);
+    bp[j] = (int8_t)((k * 5 + r16 * 11) % 23 - 11);
+  }
+  const v4i c = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, (v4i)0, 0, 0, 0);
+  int bad = 0;
+  for (int r = 0; r < 4; ++r) {
+    const int i = 4 * g + r, jj = r16;
+    int ref = 0;
+    for (int k = 0; k < 64; ++k) ref += ((i * 7 + k * 3) % 19 - 9) * ((k * 5 + jj * 11) % 23 - 11);
+    bad += ref != c[r];
+  }
+  atomicAdd(out, bad);
+}
+
+template <int HD>
+hipError_t launch_scratch_t(const fnnue_pos* pos, uint32_t n, const NetPtrs& net, uint8_t* x, int32_t* psqt,
+                            uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+  const uint32_t waves = n;
+  uint32_t blocks = (waves + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((ft_scratch_kernel<HD, 4>), dim3(blocks), dim3(256), 0, stream, pos, n, net, x, psqt, bucket, err);
+  return hipGetLastError();
+}
+
+template <int HD>
+hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups, uint32_t base, int mode,
+                           const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err,
+                           hipStream_t stream) {
+  uint32_t blocks = (ngroups + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((ft_groups_kernel<HD, 4>), dim3(blocks), dim3(256), 0, stream, pos, off, ngroups, base,
+                     mode == FNNUE_GROUP_STAR, net, x, psqt, bucket, err);
+  return hipGetLastError();
+}
+
+template <int HD>
+hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net, int32_t* positional,
+                          hipStream_t stream) {
+  const uint32_t tiles = (n + 15) / 16;
+  uint32_t blocks = (tiles + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool kernels_support_hd(uint32_t hd) {
+  return hd == 128 || hd == 256 || hd == 512 || hd == 1024 || hd == 2048;
+}
+
+#define FNNUE_HD_DISPATCH(hd, CALL) \
+  switch (hd) {                     \
+    case 128: return CALL(128);     \
+    case 256: return CALL(256);     \
+    case 512: return CALL(512);     \
+    case 1024: return CALL(1024);   \
+    case 2048: return CALL(2048);   \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_ft_scratch(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, uint8_t* x,
+                             int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+#define CALL(H) launch_scratch_t<H>(pos, n, net, x, psqt, bucket, err, stream)
+  FNNUE_HD_DISPATCH(hd, CALL)
+#undef CALL
+}
+
+hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups, uint32_t base,
+                            int mode, const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err,
+                            hipStream_t stream) {
+#define CALL(H) launch_groups_t<H>(pos, off, ngroups, base, mode, net, x, psqt, bucket, err, stream)
+  FNNUE_HD_DISPATCH(hd, CALL)
+#undef CALL
+}
+
+hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net,
+                        int32_t* positional, hipStream_t stream) {
+#define CALL(H) launch_stack_t<H>(x, bucket, n, net, positional, stream)
+  FNNUE_HD_DISPATCH(hd, CALL)
+#undef CALL
+}
+
+hipError_t run_mfma_selftest(int* bad) {
+  int* d = nullptr;
+  hipError_t e = hipMalloc(&d, sizeof(int));
+  if (e != hipSuccess) return e;
+  e = hipMemset(d, 0, sizeof(int));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(mfma_selftest_kernel, dim3(1), dim3(64), 0, 0, d);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(bad, d, sizeof(int), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  return e;
+}
+
+}  // namespace fnnue

@@ -1,0 +1,63 @@
+// net.h — .nnue file model: parser, writer, synthetic generator and the
+// contiguous device image layout shared by the host code and the kernels.
+//
+// File format follows upstream Stockfish 15.1 (SFNNv5): evaluate_nnue.cpp
+// read_header/read_parameters, nnue_feature_transformer.h read_parameters,
+// layers/affine_transform.h read_parameters, nnue_common.h (little-endian,
+// COMPRESSED_LEB128).  The pinned net is nn-ad9b42354671.nnue ([ref] build.rs:7).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace fnnue {
+
+constexpr uint32_t kVersion = 0x7AF32F20u;
+constexpr uint32_t kFtHashBase = 0x7F234CB8u;   // HalfKAv2_hm::HashValue
+constexpr uint32_t kNetHashBase = 0xEC42E90Du;  // Network::get_hash_value seed
+constexpr int kFeatures = 22528;                // 64 king sq / 2 (mirror) * 11 planes * 64
+constexpr int kPsqtBuckets = 8;
+constexpr int kStacks = 8;
+constexpr int kL2 = 16;   // FC_0_OUTPUTS + 1 (the last is the "fwd" skip output)
+constexpr int kL3 = 32;   // FC_1_OUTPUTS
+constexpr int kFc1In = 32;// 2*FC_0_OUTPUTS = 30 padded to 32
+
+uint32_t ft_hash(uint32_t hd);
+uint32_t net_hash(uint32_t hd);
+bool hd_supported(uint32_t hd);
+
+struct Stack {
+  int32_t b0[kL2];
+  std::vector<int8_t> w0;  // [kL2][hd]
+  int32_t b1[kL3];
+  int8_t w1[kL3 * kFc1In];
+  int32_t b2;
+  int8_t w2[kL3];
+};
+
+struct Net {
+  uint32_t hd = 0;
+  uint32_t file_hash = 0;
+  std::string desc;
+  std::vector<int16_t> ft_bias;   // [hd]
+  std::vector<int16_t> ft_w;      // [kFeatures][hd]
+  std::vector<int32_t> psqt_w;    // [kFeatures][kPsqtBuckets]
+  Stack st[kStacks];
+};
+
+// Returns 0 or a FNNUE_E_* code; err receives a message.
+int parse_net(const uint8_t* buf, size_t len, Net& net, std::string& err);
+void write_net(const Net& net, bool leb128, std::vector<uint8_t>& out);
+void synthesize_net(uint64_t seed, uint32_t hd, uint32_t flags, Net& net);
+
+// Device image: one contiguous buffer, sections 256-byte aligned.  The FT
+// weight table gets one extra all-zero row (index kFeatures) and the PSQT
+// table one extra zero row, used as padding targets by the gather loops.
+struct ImageLayout {
+  size_t ft_w, ft_bias, psqt_w, w0, b0, w1, b1, w2, b2, total;
+};
+ImageLayout image_layout(uint32_t hd);
+void pack_image(const Net& net, uint8_t* dst);  // dst has image_layout(hd).total bytes
+
+}  // namespace fnnue

@@ -1,0 +1,218 @@
+"""Host-side API of the MI355X NNUE evaluator over the C ABI.
+
+Mirrors what the reference does on its static-evaluation path:
+
+* ``Net.load(path)`` — ``setoption name EvalFile value <path>``
+  ([ref] src/stockfish.rs:209-211; net file from src/assets.rs:128-133).
+* ``Evaluator(net, device)`` — one engine per worker becomes one context per
+  GPU ([ref] src/stockfish.rs:23-38 ``channel``; src/main.rs:158-170).
+* ``Evaluator.eval_positions`` / ``eval_groups`` — batched replacement for one
+  ``position fen ... moves ...`` round trip per position
+  ([ref] src/stockfish.rs:274-283).
+* ``game_positions`` — the per-ply expansion of an analysis batch
+  ([ref] src/queue.rs:543-600, ``IncomingBatch::from_acquired``).
+
+Errors raise :class:`FnnueError`; the caller treats any of them as
+``PositionFailed`` for the whole batch ([ref] src/queue.rs:207-213).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+from ._native import FnnueError  # noqa: F401  (re-export)
+
+
+class Net:
+    """A parsed and validated .nnue network (immutable, shareable)."""
+
+    def __init__(self, handle: int):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def load(cls, path: str) -> "Net":
+        h = C.c_void_p()
+        N.check(N.lib.fnnue_net_load(path.encode(), C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_bytes(cls, data: bytes) -> "Net":
+        h = C.c_void_p()
+        buf = C.create_string_buffer(data, len(data))
+        N.check(N.lib.fnnue_net_load_mem(buf, len(data), C.byref(h)))
+        return cls(h.value)
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def info(self) -> tuple[int, int, str]:
+        hd, fh, desc = C.c_uint32(), C.c_uint32(), C.c_char_p()
+        N.check(N.lib.fnnue_net_info(self._h, C.byref(hd), C.byref(fh), C.byref(desc)))
+        return hd.value, fh.value, desc.value.decode(errors="replace")
+
+    def image(self) -> np.ndarray:
+        size = C.c_size_t()
+        N.check(N.lib.fnnue_net_image_size(self._h, C.byref(size)))
+        buf = np.zeros(size.value, dtype=np.uint8)
+        N.check(N.lib.fnnue_net_image_pack(self._h, N.ptr(buf), size.value))
+        return buf
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            N.lib.fnnue_net_free(self._h)
+            self._h = C.c_void_p()
+
+
+def synthesize_net(seed: int, hd: int = 1024, flags: int = 0) -> bytes:
+    """Deterministic synthetic net in the exact .nnue format."""
+    buf, size = C.c_void_p(), C.c_size_t()
+    N.check(N.lib.fnnue_net_synthesize(seed, hd, flags, C.byref(buf), C.byref(size)))
+    try:
+        return C.string_at(buf.value, size.value)
+    finally:
+        N.lib.fnnue_buffer_free(buf)
+
+
+def device_count() -> int:
+    n = C.c_int()
+    N.check(N.lib.fnnue_device_count(C.byref(n)))
+    return n.value
+
+
+class Evaluator:
+    """A net resident on one GPU (one per process/GPU)."""
+
+    def __init__(self, net: Net | None, device: int = 0, *, image_ptr: int | None = None,
+                 image_bytes: int = 0, hd: int = 0):
+        h = C.c_void_p()
+        if net is not None:
+            N.check(N.lib.fnnue_ctx_create(net.handle, device, C.byref(h)))
+        else:
+            N.check(N.lib.fnnue_ctx_create_from_image(device, hd, C.c_void_p(image_ptr), image_bytes, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def device_image(self) -> tuple[int, int]:
+        p, s = C.c_void_p(), C.c_size_t()
+        N.check(N.lib.fnnue_ctx_image(self._h, C.byref(p), C.byref(s)))
+        return p.value, s.value
+
+    def eval_positions(self, pos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
+        n = pos.shape[0]
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_eval_positions(self._h, N.ptr(pos), n, N.ptr(psqt), N.ptr(positional)))
+        return psqt, positional
+
+    def eval_groups(self, pos: np.ndarray, off: np.ndarray, mode: int = N.GROUP_CHAIN):
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = int(off[-1]) if len(off) else 0
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_eval_groups(self._h, N.ptr(pos), N.ptr(off), len(off) - 1, mode,
+                                        N.ptr(psqt), N.ptr(positional)))
+        return psqt, positional
+
+    # Device-pointer entry points (inputs resident in HBM; asynchronous).
+    def eval_positions_device(self, d_pos: int, n: int, d_psqt: int, d_positional: int, stream: int | None):
+        N.check(N.lib.fnnue_eval_positions_device(self._h, C.c_void_p(d_pos), n, C.c_void_p(d_psqt),
+                                                  C.c_void_p(d_positional), C.c_void_p(stream)))
+
+    def eval_groups_device(self, d_pos: int, d_off: int, ngroups: int, npos: int, mode: int, d_psqt: int,
+                           d_positional: int, stream: int | None):
+        N.check(N.lib.fnnue_eval_groups_device(self._h, C.c_void_p(d_pos), C.c_void_p(d_off), ngroups, npos, mode,
+                                               C.c_void_p(d_psqt), C.c_void_p(d_positional), C.c_void_p(stream)))
+
+    def check(self) -> None:
+        N.check(N.lib.fnnue_ctx_check(self._h))
+
+    def set_timing(self, enable: bool) -> None:
+        N.check(N.lib.fnnue_ctx_set_timing(self._h, 1 if enable else 0))
+
+    def timing_read(self) -> tuple[int, float, float]:
+        """(timed launches, summed feature-transformer ms, summed layer-stack ms); resets."""
+        n, a, b = C.c_uint32(), C.c_double(), C.c_double()
+        N.check(N.lib.fnnue_ctx_timing_read(self._h, C.byref(n), C.byref(a), C.byref(b)))
+        return n.value, a.value, b.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            N.lib.fnnue_ctx_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+
+def pos_from_fen(fen: str) -> np.ndarray:
+    out = N.positions_array(1)
+    N.check(N.lib.fnnue_pos_from_fen(fen.encode(), N.ptr(out)))
+    return out[0]
+
+
+def game_positions(fen: str, moves: str | list[str]) -> np.ndarray:
+    """Root + the position after every move (analysis batch expansion)."""
+    if not isinstance(moves, str):
+        moves = " ".join(moves)
+    n = C.c_size_t()
+    cap = moves.count(" ") + 2 if moves.strip() else 1
+    out = N.positions_array(cap)
+    N.check(N.lib.fnnue_game_positions(fen.encode(), moves.encode(), N.ptr(out), cap, C.byref(n)))
+    return out[: n.value]
+
+
+def game_children(fen: str, moves: str | list[str]) -> tuple[np.ndarray, np.ndarray]:
+    """Every ply plus its legal 1-ply children, as STAR groups."""
+    if not isinstance(moves, str):
+        moves = " ".join(moves)
+    nply = (moves.count(" ") + 2) if moves.strip() else 1
+    cap = nply * 256
+    out = N.positions_array(cap)
+    off = np.zeros(nply + 1, dtype=np.uint32)
+    n, g = C.c_size_t(), C.c_size_t()
+    N.check(N.lib.fnnue_game_children(fen.encode(), moves.encode(), N.ptr(out), cap, N.ptr(off), len(off),
+                                      C.byref(n), C.byref(g)))
+    return out[: n.value], off[: g.value + 1]
+
+
+def random_playouts(seed: int, count: int, min_plies: int = 0, max_plies: int = 160,
+                    mode: int = N.PLAYOUT_FINAL, threads: int = 8, cap: int | None = None):
+    """Seeded random-playout positions.  FINAL -> positions;
+    PLIES / CHILDREN -> (positions, group offsets)."""
+    if cap is None:
+        per = {N.PLAYOUT_FINAL: 1, N.PLAYOUT_PLIES: max_plies + 1, N.PLAYOUT_CHILDREN: (max_plies + 1) * 40}[mode]
+        cap = count * per
+    offcap = count * (max_plies + 1) + 1 if mode != N.PLAYOUT_FINAL else 1
+    for _ in range(2):
+        out = N.positions_array(cap)
+        off = np.zeros(offcap, dtype=np.uint32)
+        n, g = C.c_size_t(), C.c_size_t()
+        rc = N.lib.fnnue_random_playouts(seed, count, min_plies, max_plies, mode, threads, N.ptr(out), cap,
+                                         N.ptr(off), len(off), C.byref(n), C.byref(g))
+        if rc == -10 and n.value > cap:  # FNNUE_E_CAPACITY: retry with the exact size
+            cap = n.value
+            continue
+        N.check(rc)
+        break
+    if mode == N.PLAYOUT_FINAL:
+        return out[: n.value]
+    return out[: n.value], off[: g.value + 1]
+
+
+def perft(fen: str, depth: int) -> int:
+    nodes = C.c_uint64()
+    N.check(N.lib.fnnue_perft(fen.encode(), depth, C.byref(nodes)))
+    return nodes.value
+
+
+def selftest_mfma(device: int = 0) -> None:
+    N.check(N.lib.fnnue_selftest_mfma(device))

@@ -1,0 +1,179 @@
+/*
+ * fnnue.h — C ABI of the MI355X batched NNUE evaluator (libfnnue.so).
+ *
+ * This is the drop-in boundary for fishnet's static-evaluation path.  The
+ * reference has no FFI for NNUE: it drives a Stockfish child over UCI text
+ * pipes.  Each entry point below names the reference interface it replaces.
+ *
+ *   [ref] = /root/reference (schlawg/fishnet).  Upstream = Stockfish 15.1
+ *   (submodule Stockfish/, empty in the reference checkout).
+ *
+ * Conventions
+ *  - Every function returns FNNUE_OK (0) or a negative FNNUE_E_* code and then
+ *    sets a thread-local message readable with fnnue_last_error().  No aborts,
+ *    no exits.  On error no output is guaranteed (the caller maps any error to
+ *    fishnet's PositionFailed{batch_id}, [ref] src/ipc.rs:100-103,
+ *    src/queue.rs:207-213: the whole batch is dropped, never partial results).
+ *  - Host buffers are owned by the caller; device memory of a ctx is owned by
+ *    the library.  *_device entry points take device pointers and a hipStream_t
+ *    (as void*), enqueue work and return without synchronising.
+ *  - A fnnue_net is immutable and may be shared across threads; a fnnue_ctx
+ *    must not be used from two threads at once (one ctx per GPU, one process
+ *    per GPU — the analogue of one engine per worker, [ref] src/main.rs:158-170).
+ *  - Outputs per position are the two raw Stockfish NNUE terms, before
+ *    optimism / material scaling (upstream evaluate_nnue.cpp evaluate()):
+ *      psqt       = (psqtAcc[stm][bucket] - psqtAcc[~stm][bucket]) / 2
+ *      positional = Network[bucket].propagate(transformed features)
+ *    Stockfish's NNUE value is (psqt + positional) / 16 (OutputScale).
+ */
+#ifndef FNNUE_H
+#define FNNUE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FNNUE_OK 0
+#define FNNUE_E_ARG (-1)        /* bad argument (null pointer, size, mode)           */
+#define FNNUE_E_IO (-2)         /* file could not be read / written                   */
+#define FNNUE_E_FORMAT (-3)     /* .nnue version / hash / truncated / trailing bytes  */
+#define FNNUE_E_ARCH (-4)       /* architecture not supported (HD)                     */
+#define FNNUE_E_DEVICE (-5)     /* HIP runtime error or no such device                */
+#define FNNUE_E_POSITION (-6)   /* invalid position in a batch (kings, pieces, stm)   */
+#define FNNUE_E_OOM (-7)        /* host or device allocation failed                    */
+#define FNNUE_E_MOVE (-8)       /* illegal or unparsable UCI move                      */
+#define FNNUE_E_FEN (-9)        /* unparsable FEN                                      */
+#define FNNUE_E_CAPACITY (-10)  /* output buffer too small                             */
+
+typedef struct fnnue_net fnnue_net; /* parsed, validated, immutable host copy of a .nnue */
+typedef struct fnnue_ctx fnnue_ctx; /* one GPU: device-resident net + workspaces          */
+
+/* Packed position, 36 bytes.  sq[s>>1] holds square s (A1=0..H8=63) in its low
+ * nibble for even s and high nibble for odd s, as a Stockfish Piece code
+ * (W_PAWN=1..W_KING=6, B_PAWN=9..B_KING=14, 0 = empty; upstream types.h).
+ * stm: 0 = white, 1 = black.  Castling rights, en-passant square and move
+ * counters do not enter the NNUE features and are not stored. */
+typedef struct {
+  uint8_t sq[32];
+  uint8_t stm;
+  uint8_t pad[3];
+} fnnue_pos;
+
+/* ---- errors ---- */
+const char *fnnue_last_error(void);
+/* ABI version: (major << 16) | minor. */
+uint32_t fnnue_abi_version(void);
+
+/* ---- net loading ----
+ * Replaces `setoption name EvalFile value <path>` sent to the engine
+ * ([ref] src/stockfish.rs:209-211; path from src/assets.rs:128-133, 449-453;
+ * upstream evaluate_nnue.cpp load_eval/read_parameters).  Accepts plain and
+ * COMPRESSED_LEB128 tensors, checks version 0x7AF32F20, the structure hash
+ * chain and exact EOF. */
+int fnnue_net_load(const char *path, fnnue_net **out);
+int fnnue_net_load_mem(const void *buf, size_t len, fnnue_net **out);
+/* hd = TransformedFeatureDimensions (1024 for nn-ad9b42354671, [ref] build.rs:7). */
+int fnnue_net_info(const fnnue_net *net, uint32_t *hd, uint32_t *file_hash, const char **desc);
+void fnnue_net_free(fnnue_net *net);
+
+/* Deterministic synthetic net in the exact .nnue file format (the pinned net is
+ * not shipped with the reference checkout).  flags: FNNUE_SYNTH_*.  The buffer
+ * is allocated by the library; release it with fnnue_buffer_free. */
+#define FNNUE_SYNTH_LEB128 1u     /* write tensors COMPRESSED_LEB128                  */
+#define FNNUE_SYNTH_WRAP 2u       /* large FT weights: int16 accumulators wrap around */
+#define FNNUE_SYNTH_FC1_PAD 4u    /* non-zero fc_1 padding weights (inputs 30,31)      */
+int fnnue_net_synthesize(uint64_t seed, uint32_t hd, uint32_t flags, void **buf, size_t *len);
+void fnnue_buffer_free(void *buf);
+
+/* ---- device context ----
+ * Replaces spawning + initialising an engine process ([ref] src/stockfish.rs:
+ * 132-153 spawn, 203-233 init).  Uploads the net to `device` (HIP ordinal). */
+int fnnue_device_count(int *count);
+int fnnue_ctx_create(const fnnue_net *net, int device, fnnue_ctx **out);
+/* Device image of a net: one contiguous buffer, so rank 0 can RCCL-broadcast it
+ * over xGMI and the other ranks adopt it (copied into ctx-owned memory). */
+int fnnue_net_image_size(const fnnue_net *net, size_t *bytes);
+int fnnue_net_image_pack(const fnnue_net *net, void *host_buf, size_t bytes);
+int fnnue_ctx_create_from_image(int device, uint32_t hd, const void *device_image, size_t bytes, fnnue_ctx **out);
+/* Pointer to the ctx's own device image (for broadcasting from rank 0). */
+int fnnue_ctx_image(fnnue_ctx *ctx, const void **device_image, size_t *bytes);
+void fnnue_ctx_free(fnnue_ctx *ctx);
+
+/* ---- evaluation, host buffers (synchronous) ----
+ * Static eval of independent positions, accumulators from scratch.  Replaces
+ * one `position fen ... ` + eval round trip per position ([ref]
+ * src/stockfish.rs:274-283 / StockfishStub::go :44-54) with one batched call. */
+int fnnue_eval_positions(fnnue_ctx *ctx, const fnnue_pos *pos, size_t n, int32_t *psqt, int32_t *positional);
+
+/* Grouped evaluation with accumulator reuse.  Group g is pos[off[g] .. off[g+1]).
+ *  FNNUE_GROUP_CHAIN: a game's plies in order; each accumulator is derived
+ *    from the previous ply's (incremental add/sub of changed features, refresh
+ *    on own-king moves) — upstream update_accumulator along the StateInfo chain.
+ *    Feed it the expansion of an analysis batch ([ref] src/queue.rs:571-600).
+ *  FNNUE_GROUP_STAR: pos[off[g]] is a parent, the rest are its children; each
+ *    child is derived from the parent's accumulator.
+ * Results are identical to fnnue_eval_positions on the same positions. */
+#define FNNUE_GROUP_CHAIN 0
+#define FNNUE_GROUP_STAR 1
+int fnnue_eval_groups(fnnue_ctx *ctx, const fnnue_pos *pos, const uint32_t *off, size_t ngroups, int mode,
+                      int32_t *psqt, int32_t *positional);
+
+/* ---- evaluation, device buffers (asynchronous on `stream`, a hipStream_t) ----
+ * Inputs already resident in HBM; results written to device memory.  Position
+ * validity errors are latched on the device: call fnnue_ctx_check() after
+ * synchronising to turn them into FNNUE_E_POSITION. */
+int fnnue_eval_positions_device(fnnue_ctx *ctx, const fnnue_pos *d_pos, size_t n, int32_t *d_psqt,
+                                int32_t *d_positional, void *stream);
+int fnnue_eval_groups_device(fnnue_ctx *ctx, const fnnue_pos *d_pos, const uint32_t *d_off, size_t ngroups,
+                             size_t npos, int mode, int32_t *d_psqt, int32_t *d_positional, void *stream);
+/* Synchronises the ctx's device and reports (and clears) latched errors. */
+int fnnue_ctx_check(fnnue_ctx *ctx);
+
+/* ---- batch building (host) ----
+ * FEN -> packed position.  Accepts standard, X-FEN and Shredder-FEN castling. */
+int fnnue_pos_from_fen(const char *fen, fnnue_pos *out);
+/* Every position of a game: the root and the position after each move, i.e.
+ * the expansion of IncomingBatch::from_acquired for an analysis batch
+ * ([ref] src/queue.rs:543-600; moves checked for legality like
+ * Uci::to_move, :545).  `moves` is space-separated UCI (standard or Chess960
+ * castling).  Writes n_moves + 1 positions. */
+int fnnue_game_positions(const char *fen, const char *moves, fnnue_pos *out, size_t cap, size_t *n_out);
+/* Same, plus every legal 1-ply child of each position, as STAR groups:
+ * out[off[g]] is ply g, followed by its children.  off has n_groups+1 entries. */
+int fnnue_game_children(const char *fen, const char *moves, fnnue_pos *out, size_t cap, uint32_t *off,
+                        size_t off_cap, size_t *n_out, size_t *n_groups);
+/* Seeded random playouts from the start position (splitmix64; L ~ U[min,max]
+ * plies of uniformly random legal moves, stopping at mate, stalemate or the
+ * 50-move rule).  Deterministic for a given (seed, index) regardless of threads.
+ *  FNNUE_PLAYOUT_FINAL: out[i] = final position of playout i (n_out = count).
+ *  FNNUE_PLAYOUT_PLIES: every ply of every playout as CHAIN groups.
+ *  FNNUE_PLAYOUT_CHILDREN: every ply and its legal children as STAR groups.
+ * For the grouped modes off[] receives group offsets (off_cap >= groups+1). */
+#define FNNUE_PLAYOUT_FINAL 0
+#define FNNUE_PLAYOUT_PLIES 1
+#define FNNUE_PLAYOUT_CHILDREN 2
+int fnnue_random_playouts(uint64_t seed, size_t count, uint32_t min_plies, uint32_t max_plies, int mode,
+                          int threads, fnnue_pos *out, size_t cap, uint32_t *off, size_t off_cap, size_t *n_out,
+                          size_t *n_groups);
+/* perft node count (board-code self test against published known answers). */
+int fnnue_perft(const char *fen, int depth, uint64_t *nodes);
+
+/* ---- diagnostics ----
+ * Runs the int8 MFMA operand-layout self test on `device`; 0 if the hardware
+ * layout matches the kernels' assumption. */
+int fnnue_selftest_mfma(int device);
+/* Kernel timing with HIP events on the launch stream: when enabled, every
+ * chunk launched by a *_device call records events around the feature-
+ * transformer kernel and the layer-stack kernel.  fnnue_ctx_timing_read
+ * synchronises on the last event, returns the number of timed launches and the
+ * summed kernel times (ms), and resets the accumulators. */
+int fnnue_ctx_set_timing(fnnue_ctx *ctx, int enable);
+int fnnue_ctx_timing_read(fnnue_ctx *ctx, uint32_t *launches, double *ft_ms, double *stack_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FNNUE_H */

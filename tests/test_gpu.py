@@ -1,0 +1,172 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle,
+bit-exact (integer arithmetic: no tolerance).  Run on an MI355X with -m gpu."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import fishnet_amd as F
+from fishnet_amd import _native as N
+from oracle.oracle import OracleNet
+from tests.conftest import ROOT, net_bytes
+from tests.positions import FENS
+
+pytestmark = pytest.mark.gpu
+
+GAMES = json.load(open(os.path.join(ROOT, "tests", "golden", "wcc_games.json")))["games"]
+
+
+@pytest.fixture(scope="module")
+def ev_cache():
+    cache = {}
+
+    def get(seed=1, hd=1024, flags=0):
+        key = (seed, hd, flags)
+        if key not in cache:
+            data = net_bytes(seed, hd, flags)
+            cache[key] = (F.Evaluator(F.Net.from_bytes(data), 0), OracleNet(data))
+        return cache[key]
+
+    yield get
+    for ev, _ in cache.values():
+        ev.close()
+
+
+def assert_same(ev, on, pos):
+    ps, po = ev.eval_positions(pos)
+    ops, opo, rc = on.eval_packed(pos, threads=8)
+    assert rc == 0
+    bad = np.nonzero((ps != ops) | (po != opo))[0]
+    assert len(bad) == 0, f"{len(bad)} mismatches, first {bad[:5]}: gpu {ps[bad[:3]]},{po[bad[:3]]} " \
+                          f"oracle {ops[bad[:3]]},{opo[bad[:3]]}"
+
+
+def test_mfma_layout_selftest():
+    F.selftest_mfma(0)
+
+
+def test_fens_big_net(ev_cache):
+    ev, on = ev_cache()
+    pos = np.stack([F.pos_from_fen(f) for f in FENS])
+    assert_same(ev, on, pos)
+
+
+def test_random_playouts_big_net(ev_cache):
+    ev, on = ev_cache()
+    assert_same(ev, on, F.random_playouts(1, 20000, threads=8))
+
+
+@pytest.mark.parametrize("seed,hd,flags", [(7, 128, 0), (4, 256, N.SYNTH_FC1_PAD), (2, 512, N.SYNTH_LEB128),
+                                           (3, 1024, N.SYNTH_WRAP), (6, 2048, 0)])
+def test_other_nets(ev_cache, seed, hd, flags):
+    ev, on = ev_cache(seed, hd, flags)
+    assert_same(ev, on, F.random_playouts(seed + 100, 3000, threads=8))
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 65, 1000])
+def test_ragged_batch_sizes(ev_cache, n):
+    ev, on = ev_cache()
+    assert_same(ev, on, F.random_playouts(50 + n, n, threads=4))
+
+
+def test_empty_batch(ev_cache):
+    ev, _ = ev_cache()
+    ps, po = ev.eval_positions(np.zeros((0, 36), dtype=np.uint8))
+    assert len(ps) == 0 and len(po) == 0
+
+
+def test_invalid_position_fails_whole_batch(ev_cache):
+    ev, _ = ev_cache()
+    pos = F.random_playouts(5, 10, threads=2)
+    pos[3, :32] = 0  # no kings
+    with pytest.raises(F.FnnueError) as e:
+        ev.eval_positions(pos)
+    assert e.value.name == "FNNUE_E_POSITION"
+    # the ctx stays usable after the failed batch
+    ev2, on = ev_cache()
+    assert_same(ev2, on, F.random_playouts(6, 10, threads=2))
+
+
+def test_device_latched_invalid_position(ev_cache):
+    """Device-pointer path: validity is checked on the GPU and latched."""
+    import torch
+    ev, _ = ev_cache()
+    pos = F.random_playouts(5, 64, threads=2)
+    pos[10, 32] = 2  # stm out of range
+    d = torch.from_numpy(pos).cuda()
+    ps = torch.zeros(64, dtype=torch.int32, device="cuda")
+    po = torch.zeros(64, dtype=torch.int32, device="cuda")
+    ev.eval_positions_device(d.data_ptr(), 64, ps.data_ptr(), po.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    with pytest.raises(F.FnnueError) as e:
+        ev.check()
+    assert e.value.name == "FNNUE_E_POSITION"
+    ev.check()  # cleared
+
+
+def test_games_chain_incremental(ev_cache):
+    """CHAIN groups (incremental add/sub along each game) == oracle from scratch."""
+    ev, on = ev_cache()
+    pos = [F.game_positions(g["position"], g["moves"]) for g in GAMES]
+    off = np.concatenate([[0], np.cumsum([len(p) for p in pos])]).astype(np.uint32)
+    allpos = np.concatenate(pos)
+    ps, po = ev.eval_groups(allpos, off, N.GROUP_CHAIN)
+    ops, opo, rc = on.eval_packed(allpos, threads=8)
+    assert rc == 0
+    assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_random_games_chain_and_small_net(ev_cache):
+    for seed, hd in ((1, 1024), (7, 128)):
+        ev, on = ev_cache(seed, hd, 0)
+        pos, off = F.random_playouts(2, 300, mode=N.PLAYOUT_PLIES, threads=8)
+        ps, po = ev.eval_groups(pos, off, N.GROUP_CHAIN)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_children_star(ev_cache):
+    ev, on = ev_cache()
+    for g in GAMES[:3]:
+        pos, off = F.game_children(g["position"], g["moves"])
+        ps, po = ev.eval_groups(pos, off, N.GROUP_STAR)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_wrap_net_chain(ev_cache):
+    """int16 wraparound: incremental (mod 2^16) must still equal refresh."""
+    ev, on = ev_cache(3, 1024, N.SYNTH_WRAP)
+    pos, off = F.random_playouts(8, 100, mode=N.PLAYOUT_PLIES, threads=8)
+    ps, po = ev.eval_groups(pos, off, N.GROUP_CHAIN)
+    ops, opo, rc = on.eval_packed(pos, threads=8)
+    assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_full_size_properties(ev_cache):
+    """BASELINE config 2 size (1M positions): scratch == CHAIN-of-singletons
+    == STAR re-evaluation, plus a sampled oracle check."""
+    ev, on = ev_cache()
+    pos = F.random_playouts(1, 1_000_000, threads=16)
+    ps, po = ev.eval_positions(pos)
+    idx = np.random.default_rng(0).choice(len(pos), 20000, replace=False)
+    ops, opo, rc = on.eval_packed(pos[idx], threads=16)
+    assert np.array_equal(ps[idx], ops) and np.array_equal(po[idx], opo)
+    # groups of 2 in STAR mode: second = first re-derived incrementally
+    pairs = np.repeat(pos[:200_000], 2, axis=0)
+    off = np.arange(0, len(pairs) + 1, 2, dtype=np.uint32)
+    ps2, po2 = ev.eval_groups(pairs, off, N.GROUP_STAR)
+    assert np.array_equal(ps2[1::2], ps[:200_000]) and np.array_equal(po2[1::2], po[:200_000])
+
+
+def test_image_broadcast_path(ev_cache):
+    """ctx from a device image (what bench.py broadcasts over RCCL) == ctx from the net."""
+    import torch
+    ev, _ = ev_cache()
+    img = F.Net.from_bytes(net_bytes(1, 1024, 0)).image()
+    buf = torch.from_numpy(img).cuda()
+    ev2 = F.Evaluator(None, 0, image_ptr=buf.data_ptr(), image_bytes=img.size, hd=1024)
+    pos = F.random_playouts(12, 500, threads=4)
+    a, b = ev.eval_positions(pos), ev2.eval_positions(pos)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    ev2.close()
