@@ -35,6 +35,14 @@ class FnnueError(RuntimeError):
 
 
 def _load() -> C.CDLL:
+    # libfnnue.so and torch's bundled ROCm runtime share the soname
+    # libamdhip64.so.7; whichever loads first serves the whole process.  Load
+    # torch's first (when torch is installed) so that tensors allocated by
+    # torch and the library's kernels live in one HIP runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built; run `make -C fishnet_amd/csrc` or __graft_entry__.build()")
     return C.CDLL(LIB_PATH)
