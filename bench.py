@@ -42,6 +42,8 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=0, help="host threads (0 = min(16, cpu_count))")
+    ap.add_argument("--ft-impl", choices=["sliced", "gather"], default="sliced",
+                    help="feature-transformer kernel: LDS-stationary tiles (default) or per-position gather")
     return ap.parse_args()
 
 
@@ -79,6 +81,7 @@ def main():
         dist.broadcast(img, 0)
     torch.cuda.synchronize()
     ev = F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=args.hd)
+    ev.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
     del img
     t_net = time.time() - t0
 
@@ -183,6 +186,7 @@ def main():
                 "mean_pieces": round(mean_n, 3),
                 "hd": args.hd,
                 "parallelism": f"dp{world}",
+                "ft_impl": args.ft_impl,
             },
             "roofline": {
                 "bound": "hbm",
@@ -191,7 +195,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": None,
-                "kernel": "ft_scratch_kernel",
+                "kernel": "feature transformer (%s)" % ("ft_slices_kernel + plan_*" if args.ft_impl == "sliced"
+                                                         else "ft_scratch_kernel"),
                 "kernel_avg_ms": round(ft_avg_ms, 4),
                 "stack_kernel_avg_ms": round(stack_avg_ms, 4),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),

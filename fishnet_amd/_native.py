@@ -21,6 +21,7 @@ ERRORS = {
 }
 SYNTH_LEB128, SYNTH_WRAP, SYNTH_FC1_PAD = 1, 2, 4
 GROUP_CHAIN, GROUP_STAR = 0, 1
+FT_SLICED, FT_GATHER = 0, 1
 PLAYOUT_FINAL, PLAYOUT_PLIES, PLAYOUT_CHILDREN = 0, 1, 2
 POS_BYTES = 36
 
@@ -81,6 +82,7 @@ SIGNATURES = {
     "fnnue_perft": ([C.c_char_p, _i32, _P(_u64)], _i32),
     "fnnue_selftest_mfma": ([_i32], _i32),
     "fnnue_ctx_set_timing": ([_vp, _i32], _i32),
+    "fnnue_ctx_set_ft_impl": ([_vp, _i32], _i32),
     "fnnue_ctx_timing_read": ([_vp, _P(_u32), _P(C.c_double), _P(C.c_double)], _i32),
 }
 

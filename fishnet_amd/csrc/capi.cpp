@@ -7,6 +7,7 @@
 #include <array>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -67,6 +68,8 @@ struct fnnue_ctx {
   int32_t* d_psqt = nullptr;
   int32_t* d_positional = nullptr;
   size_t stage_cap = 0, off_cap = 0;
+  int ft_impl = FNNUE_FT_SLICED;
+  SlicedPlan plan{};
   bool timing = false;
   std::vector<std::array<hipEvent_t, 3>> evpool;  // per timed launch: before ft, between, after stack
   size_t evused = 0;
@@ -93,7 +96,8 @@ void ctx_destroy(fnnue_ctx* c) {
       if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off,
-                  (void*)c->d_psqt, (void*)c->d_positional})
+                  (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
+                  (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm})
     if (p) (void)hipFree(p);
   delete c;
 }
@@ -132,6 +136,16 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
   if (hipMalloc(&c->bucket, kChunk) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
   if (hipMalloc(&c->err, sizeof(uint32_t)) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (error word)");
   HIP_TRY(hipMemset(c->err, 0, sizeof(uint32_t)), "hipMemset");
+  SlicedPlan& P = c->plan;
+  if (hipMalloc(&P.tiles, sliced_tiles_bytes(hd)) != hipSuccess ||
+      hipMalloc(&P.ctr, sliced_ctr_words() * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.units, (size_t)sliced_max_units(kChunk) * 16) != hipSuccess ||
+      hipMalloc(&P.items, (size_t)2 * kChunk * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.flist, (size_t)2 * kChunk * 32 * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&P.perm, (size_t)kChunk * sizeof(uint32_t)) != hipSuccess)
+    return fail(FNNUE_E_OOM, "device allocation (sliced plan)");
+  if (const char* impl = std::getenv("FNNUE_FT_IMPL"))
+    c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
   c->ptrs = make_ptrs(c->image, hd);
   *out = c.release();
@@ -186,6 +200,13 @@ bool valid_host_pos(const fnnue_pos& p) {
   return wk == 1 && bk == 1 && n <= 32 && p.stm <= 1;
 }
 
+// Derives the LDS-tile layout of the FT weights from the (just uploaded) image.
+int finish_upload(fnnue_ctx* c) {
+  HIP_TRY(launch_relayout_sliced(c->hd, c->ptrs, c->plan.tiles, c->stream), "relayout launch");
+  HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  return FNNUE_OK;
+}
+
 // Timing events for the next launch (grown on demand, reused after a read).
 int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
   *out = nullptr;
@@ -200,9 +221,10 @@ int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
 }
 
 // Runs the stack kernel for [0, n) of the workspace and records timing.
-int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 3>* ev) {
+int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 3>* ev,
+                   const uint32_t* perm = nullptr) {
   if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
-  HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, s), "stack kernel launch");
+  HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, perm, s), "stack kernel launch");
   if (ev) HIP_TRY(hipEventRecord((*ev)[2], s), "hipEventRecord");
   return FNNUE_OK;
 }
@@ -313,6 +335,10 @@ int fnnue_ctx_create(const fnnue_net* net, int device, fnnue_ctx** out) {
     ctx_destroy(c);
     return hip_fail(e, "hipMemcpy(net image)");
   }
+  if ((rc = finish_upload(c)) != FNNUE_OK) {
+    ctx_destroy(c);
+    return rc;
+  }
   *out = c;
   return FNNUE_OK;
 }
@@ -330,6 +356,10 @@ int fnnue_ctx_create_from_image(int device, uint32_t hd, const void* device_imag
     ctx_destroy(c);
     return hip_fail(e, "hipMemcpy(device image)");
   }
+  if ((rc = finish_upload(c)) != FNNUE_OK) {
+    ctx_destroy(c);
+    return rc;
+  }
   *out = c;
   return FNNUE_OK;
 }
@@ -342,6 +372,12 @@ int fnnue_ctx_image(fnnue_ctx* ctx, const void** device_image, size_t* bytes) {
 }
 
 void fnnue_ctx_free(fnnue_ctx* ctx) { ctx_destroy(ctx); }
+
+int fnnue_ctx_set_ft_impl(fnnue_ctx* ctx, int impl) {
+  if (!ctx || (impl != FNNUE_FT_SLICED && impl != FNNUE_FT_GATHER)) return fail(FNNUE_E_ARG, "bad ft impl");
+  ctx->ft_impl = impl;
+  return FNNUE_OK;
+}
 
 int fnnue_ctx_set_timing(fnnue_ctx* ctx, int enable) {
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
@@ -382,9 +418,17 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
     int rc = next_events(ctx, &ev);
     if (rc) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
-    HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
-            "ft_scratch launch");
-    rc = run_chunk_tail(ctx, m, d_positional + b, s, ev);
+    const uint32_t* perm = nullptr;
+    if (ctx->ft_impl == FNNUE_FT_GATHER) {
+      HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
+              "ft_scratch launch");
+    } else {
+      HIP_TRY(launch_ft_sliced(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->plan, ctx->x, d_psqt + b, ctx->bucket,
+                               ctx->err, s),
+              "ft_sliced launch");
+      perm = ctx->plan.perm;
+    }
+    rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, perm);
     if (rc) return rc;
   }
   return FNNUE_OK;

@@ -1,0 +1,383 @@
+// ft_sliced.hip — LDS-stationary feature transformer for batches of
+// independent positions (BASELINE config 2, "from scratch").
+//
+// Why: a position's two accumulators need 2n rows of 2 KiB gathered from a
+// 46 MB table (HD = 1024).  Gathered per position (ft_scratch_kernel) the rows
+// come from L2 (~72 % hits) and the Infinity Cache at ~22 TB/s.  Here the
+// table is instead split into (king block kb, slice s) tiles of 705 rows x
+// 128 B (64 of the HD int16 columns: 32 from each half, so the pairwise
+// product stays inside a tile); one 1024-thread workgroup holds one tile in
+// LDS (90 KB of the CU's 160 KB) and streams every perspective-item whose
+// king block is kb through it, reading rows with ds_read_b128.  HBM/L2 then
+// see only the compact plan (feature lists) and the transformed output.
+//
+// Pipeline per chunk of positions (all on the caller's stream, no host sync):
+//   plan_count    per-workgroup LDS histograms of item keys (kb, n) and of
+//                 position buckets -> global counts
+//   plan_scan     one workgroup: exclusive scans -> item / slot offsets, and
+//                 the unit table (kb, item range of <= kUnitItems)
+//   plan_scatter  counting-sort scatter: per item its 32 feature rows (u16,
+//                 relative to kb, padded with the zero row) and its output
+//                 slot; positions re-ordered by layer-stack bucket; PSQT term
+//   ft_slices     (unit, slice) workgroups, XCD-aware: all slices of a unit
+//                 run on one XCD so the unit's feature lists are read once
+//                 into that XCD's L2
+// then stack_kernel (kernels.hip) over the bucket-sorted slots.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "kernels.h"
+#include "net.h"
+
+namespace fnnue {
+
+namespace {
+
+constexpr int kRowsPerBlock = 704;            // PS_NB: rows per king block
+constexpr int kTileRows = kRowsPerBlock + 1;  // + one zero row
+constexpr int kNoRow = kRowsPerBlock;         // padding entry -> zero row
+constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
+constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
+constexpr int kBins = kItemBins + kPosBins;
+constexpr int kScatterPositions = 512;        // positions per plan_scatter workgroup
+
+// Counter block layout (uint32 words).
+constexpr int kCnt = 0, kOff = kBins, kCur = 2 * kBins, kNUnits = 3 * kBins;
+
+// ds_read_b128 services a wave in four 16-lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32).  Give each group exactly two items of 8 lanes so
+// a group touches two 128-B rows (at most a 2-way bank conflict).
+__device__ __forceinline__ void lane_item(int lane, int& item, int& q) {
+  const int l = lane & 31, hi = (lane >> 5) * 4;
+  if (l < 4) { item = 0; q = l; }
+  else if (l < 12) { item = 2; q = l - 4; }
+  else if (l < 16) { item = 0; q = l - 8; }
+  else if (l < 20) { item = 3; q = l - 16; }
+  else if (l < 28) { item = 1; q = l - 20; }
+  else { item = 3; q = l - 24; }
+  item += hi;
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void plan_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                                         uint32_t* __restrict__ ctr, uint32_t* __restrict__ err) {
+  __shared__ uint32_t h[kBins];
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < n; p += nw) {
+    const Decoded d = decode(pos + p, lane);
+    if (lane == 0) {
+      if (!d.ok) {
+        atomicOr(err, 1u);
+        atomicAdd(&h[kItemBins + 8], 1u);
+      } else {
+        atomicAdd(&h[king_block(0, d.wk) * 33 + d.cnt], 1u);
+        atomicAdd(&h[king_block(1, d.bk) * 33 + d.cnt], 1u);
+        atomicAdd(&h[kItemBins + ((d.cnt - 1) >> 2)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&ctr[kCnt + i], h[i]);
+}
+
+// One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ ctr, int4* __restrict__ units,
+                                                         uint32_t unit_items) {
+  __shared__ uint32_t s[kBins];
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  // Exclusive scan of the item bins and, separately, of the position bins.
+  constexpr int per = (kBins + 1023) / 1024;
+  uint32_t local[per];
+  uint32_t sum = 0;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    local[k] = (i < kItemBins) ? ctr[kCnt + i] : 0;
+    sum += local[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i < kItemBins) s[i] = run;
+    run += local[k];
+  }
+  if (t == 0) {
+    uint32_t r = 0;
+    for (int b = 0; b < kPosBins; ++b) {
+      s[kItemBins + b] = r;
+      r += ctr[kCnt + kItemBins + b];
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < kBins; i += 1024) {
+    ctr[kOff + i] = s[i];
+    ctr[kCur + i] = s[i];
+  }
+  if (t == 0) {
+    // Unit table: each king block's item range in chunks of <= unit_items.
+    uint32_t nu = 0;
+    for (int kb = 0; kb < 32; ++kb) {
+      const uint32_t b = s[kb * 33];
+      const uint32_t e = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
+      for (uint32_t c = b; c < e; c += unit_items) units[nu++] = make_int4(kb, (int)c, (int)min(e, c + unit_items), 0);
+    }
+    ctr[kNUnits] = nu;
+  }
+}
+
+// Item record: (n << 24) | (slot << 1) | half, half 0 = side-to-move half of x.
+__global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                                           const int32_t* __restrict__ psqw,
+                                                           uint32_t* __restrict__ ctr, uint32_t* __restrict__ items,
+                                                           uint16_t* __restrict__ flist, uint32_t* __restrict__ perm,
+                                                           uint8_t* __restrict__ bucket_out,
+                                                           int32_t* __restrict__ psqt_out) {
+  __shared__ uint32_t lcnt[kBins];
+  __shared__ uint32_t lbase[kBins];
+  __shared__ uint16_t rank[3][kScatterPositions];
+  __shared__ uint16_t rows[4][2][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t p0 = blockIdx.x * kScatterPositions;
+  const uint32_t pend = min(n, p0 + kScatterPositions);
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x) lcnt[i] = 0;
+  __syncthreads();
+  // Pass A: local ranks.
+  for (uint32_t p = p0 + wv; p < pend; p += 4) {
+    const Decoded d = decode(pos + p, lane);
+    if (lane == 0) {
+      const uint32_t lp = p - p0;
+      if (d.ok) {
+        rank[0][lp] = (uint16_t)atomicAdd(&lcnt[king_block(0, d.wk) * 33 + d.cnt], 1u);
+        rank[1][lp] = (uint16_t)atomicAdd(&lcnt[king_block(1, d.bk) * 33 + d.cnt], 1u);
+        rank[2][lp] = (uint16_t)atomicAdd(&lcnt[kItemBins + ((d.cnt - 1) >> 2)], 1u);
+      } else {
+        rank[2][lp] = (uint16_t)atomicAdd(&lcnt[kItemBins + 8], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  // Reserve this workgroup's range in every bin it uses.
+  for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+    lbase[i] = lcnt[i] ? atomicAdd(&ctr[kCur + i], lcnt[i]) : 0;
+  __syncthreads();
+  // Pass B: scatter.
+  for (uint32_t p = p0 + wv; p < pend; p += 4) {
+    const Decoded d = decode(pos + p, lane);
+    const uint32_t lp = p - p0;
+    if (!d.ok) {
+      if (lane == 0) {
+        const uint32_t slot = lbase[kItemBins + 8] + rank[2][lp];
+        perm[slot] = p;
+        bucket_out[slot] = 0xFF;
+        psqt_out[p] = 0;
+      }
+      continue;
+    }
+    const int bucket = (d.cnt - 1) >> 2;
+    const uint32_t slot = lbase[kItemBins + bucket] + rank[2][lp];
+    const int kbw = king_block(0, d.wk), kbb = king_block(1, d.bk);
+    const uint32_t iw = lbase[kbw * 33 + d.cnt] + rank[0][lp];
+    const uint32_t ib = lbase[kbb * 33 + d.cnt] + rank[1][lp];
+    int fw = kZeroRow, fb = kZeroRow;
+    if (d.pc) {
+      fw = make_index(0, lane, d.pc, d.wk);
+      fb = make_index(1, lane, d.pc, d.bk);
+      // compact the rows (relative to the king block) in square order
+      const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(d.occ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)d.occ, 0));
+      rows[wv][0][r] = (uint16_t)(fw - kRowsPerBlock * kbw);
+      rows[wv][1][r] = (uint16_t)(fb - kRowsPerBlock * kbb);
+    }
+    const int v = psqw[fw * kPsqtBuckets + bucket] - psqw[fb * kPsqtBuckets + bucket];
+    int tot = wave_sum(v);
+    if (d.stm) tot = -tot;
+    wave_lds_sync();
+    const int persp = lane >> 5, k = lane & 31;
+    const uint16_t e = k < d.cnt ? rows[wv][persp][k] : (uint16_t)kNoRow;
+    flist[(size_t)(persp ? ib : iw) * 32 + k] = e;
+    wave_lds_sync();
+    if (lane == 0) {
+      items[iw] = ((uint32_t)d.cnt << 24) | (slot << 1) | (uint32_t)(d.stm != 0);
+      items[ib] = ((uint32_t)d.cnt << 24) | (slot << 1) | (uint32_t)(d.stm != 1);
+      perm[slot] = p;
+      bucket_out[slot] = (uint8_t)bucket;
+      psqt_out[p] = tot / 2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tile image: tile(kb, s)[r][q] (16 B) = {ft_w[kb*704+r][32s+4q .. +3],
+// ft_w[kb*704+r][HD/2+32s+4q .. +3]}, r = 704 is the zero row.
+template <int HD>
+__global__ __launch_bounds__(256) void relayout_kernel(const int16_t* __restrict__ ftw, uint4* __restrict__ tiles) {
+  constexpr int S = HD / 64;
+  const size_t total = (size_t)32 * S * kTileRows * 8;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int q = i & 7;
+    const size_t t = i >> 3;
+    const int r = (int)(t % kTileRows);
+    const size_t ks = t / kTileRows;
+    const int s = (int)(ks % S), kb = (int)(ks / S);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < kRowsPerBlock) {
+      const int16_t* row = ftw + (size_t)(kb * kRowsPerBlock + r) * HD;
+      const uint2 lo = *reinterpret_cast<const uint2*>(row + 32 * s + 4 * q);
+      const uint2 hi = *reinterpret_cast<const uint2*>(row + HD / 2 + 32 * s + 4 * q);
+      v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+    tiles[i] = v;
+  }
+}
+
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t transform4(u16x4 lo, u16x4 hi) {
+  const s16x4 zero = (s16x4)0, top = (s16x4)127;
+  const s16x4 a = __builtin_elementwise_min(__builtin_elementwise_max((s16x4)lo, zero), top);
+  const s16x4 b = __builtin_elementwise_min(__builtin_elementwise_max((s16x4)hi, zero), top);
+  const u16x4 pr = ((u16x4)a * (u16x4)b) >> (u16x4)7;
+  return (uint32_t)pr.x | ((uint32_t)pr.y << 8) | ((uint32_t)pr.z << 16) | ((uint32_t)pr.w << 24);
+}
+
+// One workgroup = one (unit, slice).  16 waves x 8 items per pass.
+template <int HD>
+__global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict__ tiles,
+                                                         const int16_t* __restrict__ ftb,
+                                                         const uint32_t* __restrict__ ctr,
+                                                         const int4* __restrict__ units,
+                                                         const uint32_t* __restrict__ items,
+                                                         const uint16_t* __restrict__ flist,
+                                                         uint8_t* __restrict__ x) {
+  constexpr int S = HD / 64;
+  __shared__ uint4 img[kTileRows * 8];
+  const uint32_t w = blockIdx.x;
+  const uint32_t j = w >> 3;
+  const uint32_t unit = (j / S) * 8 + (w & 7);
+  const int s = (int)(j % S);
+  if (unit >= ctr[kNUnits]) return;
+  const int4 u = units[unit];
+  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileRows * 8;
+  for (int i = threadIdx.x; i < kTileRows * 8; i += 1024) img[i] = src[i];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int it_in_wave, q;
+  lane_item(lane, it_in_wave, q);
+  const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
+  const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+  __syncthreads();
+  for (int base = u.y + wv * 8; base < u.z; base += 16 * 8) {
+    const int it = base + it_in_wave;
+    const bool valid = it < u.z;
+    const uint32_t rec = valid ? items[it] : 0;
+    const int ni = (int)(rec >> 24);
+    int maxn = ni;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) maxn = max(maxn, __shfl_xor(maxn, o));
+    uint32_t e[16];
+    if (valid) {
+      const uint4* fl = reinterpret_cast<const uint4*>(flist + (size_t)it * 32);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 v = fl[k];
+        e[4 * k] = v.x; e[4 * k + 1] = v.y; e[4 * k + 2] = v.z; e[4 * k + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) e[k] = (uint32_t)kNoRow * 0x10001u;
+    }
+    u16x4 lo = b_lo, hi = b_hi;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      if (4 * g < maxn) {
+        uint4 v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t word = e[2 * g + (t >> 1)];
+          const uint32_t r = (t & 1) ? (word >> 16) : (word & 0xFFFF);
+          v[t] = img[r * 8 + q];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          lo += __builtin_bit_cast(u16x4, make_uint2(v[t].x, v[t].y));
+          hi += __builtin_bit_cast(u16x4, make_uint2(v[t].z, v[t].w));
+        }
+      }
+    }
+    if (valid) {
+      const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
+      *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
+    }
+  }
+}
+
+template <int HD>
+hipError_t relayout_t(const NetPtrs& net, void* tiles, hipStream_t stream) {
+  hipLaunchKernelGGL((relayout_kernel<HD>), dim3(2048), dim3(256), 0, stream, net.ft_w, (uint4*)tiles);
+  return hipGetLastError();
+}
+
+template <int HD>
+hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint32_t max_units, hipStream_t stream) {
+  constexpr int S = HD / 64;
+  const uint32_t groups = (max_units + 7) / 8;
+  hipLaunchKernelGGL((ft_slices_kernel<HD>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+                     (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, x);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t sliced_tiles_bytes(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileRows * 16; }
+size_t sliced_ctr_words() { return 3 * kBins + 16; }
+uint32_t sliced_max_units(uint32_t chunk) { return 32 + (2 * chunk + kUnitItems - 1) / kUnitItems; }
+
+#define FNNUE_HD_DISPATCH(hd, CALL) \
+  switch (hd) {                     \
+    case 128: return CALL(128);     \
+    case 256: return CALL(256);     \
+    case 512: return CALL(512);     \
+    case 1024: return CALL(1024);   \
+    case 2048: return CALL(2048);   \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_relayout_sliced(uint32_t hd, const NetPtrs& net, void* tiles, hipStream_t stream) {
+#define CALL(H) relayout_t<H>(net, tiles, stream)
+  FNNUE_HD_DISPATCH(hd, CALL)
+#undef CALL
+}
+
+hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
+                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  const uint32_t waves = n;
+  uint32_t blocks = (waves + 3) / 4;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(plan_count_kernel, dim3(blocks), dim3(256), 0, stream, pos, n, P.ctr, err);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(plan_scatter_kernel, dim3((n + kScatterPositions - 1) / kScatterPositions), dim3(256), 0, stream,
+                     pos, n, net.psqt_w, P.ctr, P.items, P.flist, P.perm, bucket, psqt);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint32_t mu = sliced_max_units(n);
+#define CALL(H) ft_slices_t<H>(P, net, x, mu, stream)
+  FNNUE_HD_DISPATCH(hd, CALL)
+#undef CALL
+}
+
+}  // namespace fnnue

@@ -31,9 +31,28 @@ hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* o
                             uint32_t base, int mode, const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket,
                             uint32_t* err, hipStream_t stream);
 
-// Layer stacks: 16 positions per wave, int8 MFMA for fc_0 and fc_1.
+// Layer stacks: 16 positions per wave, int8 MFMA for fc_0 and fc_1.  Row i of
+// x / bucket is written to positional[perm ? perm[i] : i].
 hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net,
-                        int32_t* positional, hipStream_t stream);
+                        int32_t* positional, const uint32_t* perm, hipStream_t stream);
+
+// LDS-stationary feature transformer (ft_sliced.hip).
+constexpr uint32_t kUnitItems = 2048;  // perspective-items per (king block) work unit
+struct SlicedPlan {
+  void* tiles;       // [32 king blocks][hd/64 slices][705 rows][8] x 16 B (relayout of ft_w)
+  uint32_t* ctr;     // sliced_ctr_words() counters / offsets
+  void* units;       // int4 [sliced_max_units(chunk)]
+  uint32_t* items;   // [2 * chunk] item records
+  uint16_t* flist;   // [2 * chunk][32] feature rows relative to the king block
+  uint32_t* perm;    // [chunk] bucket-sorted slot -> position index
+};
+size_t sliced_tiles_bytes(uint32_t hd);
+size_t sliced_ctr_words();
+uint32_t sliced_max_units(uint32_t chunk);
+hipError_t launch_relayout_sliced(uint32_t hd, const NetPtrs& net, void* tiles, hipStream_t stream);
+// Writes psqt[pos], x[slot], bucket[slot] and P.perm; then run launch_stack with P.perm.
+hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
+                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream);
 
 // MFMA operand-layout self test: returns number of mismatching outputs in *bad.
 hipError_t run_mfma_selftest(int* bad);

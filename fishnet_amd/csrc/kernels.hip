@@ -19,70 +19,13 @@
 // bit-exact regardless of scheduling.
 #include <hip/hip_runtime.h>
 
+#include "device_common.h"
 #include "kernels.h"
 #include "net.h"
 
 namespace fnnue {
 
 namespace {
-
-constexpr int kZeroRow = kFeatures;  // all-zero padding row in ft_w / psqt_w
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-template <int N> struct Vec {
-  typedef unsigned short u16 __attribute__((ext_vector_type(N)));
-  typedef short s16 __attribute__((ext_vector_type(N)));
-  typedef unsigned char u8 __attribute__((ext_vector_type(N)));
-};
-
-// HalfKAv2_hm::make_index (upstream features/half_ka_v2_hm.cpp):
-//   orient(p, s, ksq) = s ^ (p * SQ_A8) ^ ((file_of(ksq) < FILE_E) * SQ_H1)
-//   index = orient(s) + PieceSquareIndex[p][pc] + PS_NB * KingBuckets[orient(ksq)]
-// KingBuckets[o] = 4*(7-rank(o)) + (7-file(o)) for the e..h files o lands on.
-__device__ __forceinline__ int make_index(int persp, int s, int pc, int ksq) {
-  const int flip = (persp ? 56 : 0) ^ (((ksq & 7) < 4) ? 7 : 0);
-  const int os = s ^ flip, ok = ksq ^ flip;
-  const int type = pc & 7;
-  const int plane = type == 6 ? 10 : 2 * (type - 1) + ((pc >> 3) != persp);
-  return os + 64 * plane + 704 * (4 * (7 - (ok >> 3)) + (7 - (ok & 7)));
-}
-
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Decoded position as seen by one wave: lane l = square l.
-struct Decoded {
-  int pc;        // piece on this lane's square
-  uint64_t occ;  // occupied squares
-  int stm, wk, bk, cnt;
-  bool ok;
-};
-
-__device__ __forceinline__ Decoded decode(const fnnue_pos* p, int lane) {
-  Decoded d;
-  const uint8_t* pp = reinterpret_cast<const uint8_t*>(p);
-  const int byte = pp[lane >> 1];
-  d.pc = (byte >> ((lane & 1) * 4)) & 15;
-  d.stm = pp[32];
-  d.occ = __ballot(d.pc != 0);
-  const uint64_t wkm = __ballot(d.pc == 6), bkm = __ballot(d.pc == 14);
-  const uint64_t bad = __ballot(d.pc == 7 || d.pc == 8 || d.pc == 15);
-  d.cnt = __popcll(d.occ);
-  d.ok = !bad && __popcll(wkm) == 1 && __popcll(bkm) == 1 && d.cnt <= 32 && d.stm <= 1;
-  d.wk = wkm ? __builtin_ctzll(wkm) : 0;
-  d.bk = bkm ? __builtin_ctzll(bkm) : 0;
-  return d;
-}
 
 // FeatureTransformer::transform for one perspective half (upstream
 // nnue_feature_transformer.h): out[j] = clamp(a[j],0,127) * clamp(a[j+HD/2],0,127) / 128.
@@ -364,7 +307,8 @@ __device__ __forceinline__ int sqr_crelu(int v) {
 
 template <int HD>
 __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ bucket,
-                                                    uint32_t n, NetPtrs net, int32_t* __restrict__ positional) {
+                                                    uint32_t n, NetPtrs net, int32_t* __restrict__ positional,
+                                                    const uint32_t* __restrict__ perm) {
   constexpr int KS = HD / 64;
   __shared__ __attribute__((aligned(16))) uint8_t x1s[4][16][64];
   __shared__ int32_t fwds[4][16];
@@ -380,6 +324,7 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
     const uint32_t prow = p0 + r16;
     const bool row_ok = prow < n;
     const int bk = row_ok ? bucket[prow] : 0xFF;
+    if (row_ok && bk == 0xFF && g == 0) positional[perm ? perm[prow] : prow] = 0;  // invalid position
     uint32_t bmask = 0;
 #pragma unroll
     for (int b = 0; b < kStacks; ++b)
@@ -431,7 +376,7 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
       for (int r = 0; r < 4; ++r) {
         const int p = 4 * g + r;
         const int pb = __shfl(bk, p);
-        if (r16 == 0 && pb == b) positional[p0 + p] = b2 + part[r] + fwds[wv][p];
+        if (r16 == 0 && pb == b) positional[perm ? perm[p0 + p] : p0 + p] = b2 + part[r] + fwds[wv][p];
       }
       wave_lds_sync();
     }
@@ -487,12 +432,12 @@ hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t n
 
 template <int HD>
 hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net, int32_t* positional,
-                          hipStream_t stream) {
+                          const uint32_t* perm, hipStream_t stream) {
   const uint32_t tiles = (n + 15) / 16;
   uint32_t blocks = (tiles + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional);
+  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional, perm);
   return hipGetLastError();
 }
 
@@ -528,8 +473,8 @@ hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* o
 }
 
 hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net,
-                        int32_t* positional, hipStream_t stream) {
-#define CALL(H) launch_stack_t<H>(x, bucket, n, net, positional, stream)
+                        int32_t* positional, const uint32_t* perm, hipStream_t stream) {
+#define CALL(H) launch_stack_t<H>(x, bucket, n, net, positional, perm, stream)
   FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
 }

@@ -135,6 +135,10 @@ class Evaluator:
     def check(self) -> None:
         N.check(N.lib.fnnue_ctx_check(self._h))
 
+    def set_ft_impl(self, impl: int) -> None:
+        """FT_SLICED (default, LDS-stationary tiles) or FT_GATHER (per-position row gather)."""
+        N.check(N.lib.fnnue_ctx_set_ft_impl(self._h, impl))
+
     def set_timing(self, enable: bool) -> None:
         N.check(N.lib.fnnue_ctx_set_timing(self._h, 1 if enable else 0))
 

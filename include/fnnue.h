@@ -165,6 +165,16 @@ int fnnue_perft(const char *fen, int depth, uint64_t *nodes);
  * Runs the int8 MFMA operand-layout self test on `device`; 0 if the hardware
  * layout matches the kernels' assumption. */
 int fnnue_selftest_mfma(int device);
+/* Feature-transformer implementation for fnnue_eval_positions*:
+ *  FNNUE_FT_SLICED (default): LDS-stationary weight tiles, positions planned
+ *    and sorted on the device.
+ *  FNNUE_FT_GATHER: one wave per position gathering rows from L2/HBM.
+ * Both are bit-identical; the environment variable FNNUE_FT_IMPL=gather|sliced
+ * sets the default for new contexts. */
+#define FNNUE_FT_SLICED 0
+#define FNNUE_FT_GATHER 1
+int fnnue_ctx_set_ft_impl(fnnue_ctx *ctx, int impl);
+
 /* Kernel timing with HIP events on the launch stream: when enabled, every
  * chunk launched by a *_device call records events around the feature-
  * transformer kernel and the layer-stack kernel.  fnnue_ctx_timing_read

@@ -64,10 +64,39 @@ def test_other_nets(ev_cache, seed, hd, flags):
     assert_same(ev, on, F.random_playouts(seed + 100, 3000, threads=8))
 
 
-@pytest.mark.parametrize("n", [1, 15, 16, 17, 63, 65, 1000])
-def test_ragged_batch_sizes(ev_cache, n):
+@pytest.mark.parametrize("impl", [N.FT_SLICED, N.FT_GATHER])
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 65, 1000, 2049, 4097])
+def test_ragged_batch_sizes(ev_cache, n, impl):
     ev, on = ev_cache()
-    assert_same(ev, on, F.random_playouts(50 + n, n, threads=4))
+    ev.set_ft_impl(impl)
+    try:
+        assert_same(ev, on, F.random_playouts(50 + n, n, threads=4))
+    finally:
+        ev.set_ft_impl(N.FT_SLICED)
+
+
+@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (3, 1024, N.SYNTH_WRAP), (6, 2048, 0)])
+def test_ft_impls_agree(ev_cache, seed, hd, flags):
+    """LDS-stationary (sliced) and per-position gather feature transformers."""
+    ev, on = ev_cache(seed, hd, flags)
+    pos = F.random_playouts(seed + 7, 50000, threads=8)
+    a = ev.eval_positions(pos)
+    ev.set_ft_impl(N.FT_GATHER)
+    b = ev.eval_positions(pos)
+    ev.set_ft_impl(N.FT_SLICED)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    idx = np.arange(0, len(pos), 7)
+    ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+    assert np.array_equal(a[0][idx], ops) and np.array_equal(a[1][idx], opo)
+
+
+def test_same_king_block_everywhere(ev_cache):
+    """Degenerate plan: every item in one king block / one n bin (one huge bin,
+    many units for a single tile)."""
+    ev, on = ev_cache()
+    start = F.pos_from_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1")
+    pos = np.repeat(start[None, :], 10000, axis=0)
+    assert_same(ev, on, pos)
 
 
 def test_empty_batch(ev_cache):
@@ -80,6 +109,11 @@ def test_invalid_position_fails_whole_batch(ev_cache):
     ev, _ = ev_cache()
     pos = F.random_playouts(5, 10, threads=2)
     pos[3, :32] = 0  # no kings
+    with pytest.raises(F.FnnueError) as e:
+        ev.eval_positions(pos)
+    assert e.value.name == "FNNUE_E_POSITION"
+    pos = F.random_playouts(5, 10, threads=2)
+    pos[4, 0] = (pos[4, 0] & 0xF0) | 7  # invalid piece code 7 on a1
     with pytest.raises(F.FnnueError) as e:
         ev.eval_positions(pos)
     assert e.value.name == "FNNUE_E_POSITION"
