@@ -53,10 +53,9 @@ def main():
     import torch.distributed as dist
 
     import fishnet_amd as F
+    from fishnet_amd import dist as D
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = D.env_rank()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     threads = args.threads or min(16, os.cpu_count() or 1)
@@ -68,17 +67,11 @@ def main():
 
     # ---- net: synthesized on rank 0, device image broadcast over RCCL/xGMI ----
     t0 = time.time()
-    if rank == 0:
-        net = F.Net.from_bytes(F.synthesize_net(args.seed, args.hd, 0))
-        img = torch.from_numpy(net.image()).cuda()
-        size = torch.tensor([img.numel()], dtype=torch.int64, device="cuda")
-    else:
-        size = torch.zeros(1, dtype=torch.int64, device="cuda")
+    image = F.Net.from_bytes(F.synthesize_net(args.seed, args.hd, 0)).image() if rank == 0 else None
     if dist_on:
-        dist.broadcast(size, 0)
-        if rank != 0:
-            img = torch.empty(int(size.item()), dtype=torch.uint8, device="cuda")
-        dist.broadcast(img, 0)
+        img = D.broadcast_image(image, torch.device("cuda", local))
+    else:
+        img = torch.from_numpy(image).cuda()
     torch.cuda.synchronize()
     ev = F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=args.hd)
     ev.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
@@ -87,8 +80,7 @@ def main():
 
     # ---- inputs: this rank's shard of random-playout positions, resident in HBM ----
     t0 = time.time()
-    shard_seed = args.seed + 1_000_003 * rank
-    pos = F.random_playouts(shard_seed, args.positions, 0, 160, threads=threads)
+    pos = F.random_playouts(D.shard_seed(args.seed, rank), args.positions, 0, 160, threads=threads)
     t_gen = time.time() - t0
     board = np.zeros((len(pos), 64), dtype=np.uint8)
     board[:, 0::2] = pos[:, :32] & 15
@@ -124,10 +116,7 @@ def main():
     ev.set_timing(False)
     ev.check()
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if dist_on:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed_max = float(el.item())
+    elapsed_max = D.max_over_ranks(elapsed, torch.device("cuda", local)) if dist_on else elapsed
     total_positions = args.positions * world * args.steps
     value = total_positions / elapsed_max
 

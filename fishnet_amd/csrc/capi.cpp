@@ -202,6 +202,10 @@ bool valid_host_pos(const fnnue_pos& p) {
 
 // Derives the LDS-tile layout of the FT weights from the (just uploaded) image.
 int finish_upload(fnnue_ctx* c) {
+  if (std::getenv("FNNUE_DEBUG_SKIP_RELAYOUT")) {  // diagnostics only: gather path without tiles
+    c->ft_impl = FNNUE_FT_GATHER;
+    return FNNUE_OK;
+  }
   HIP_TRY(launch_relayout_sliced(c->hd, c->ptrs, c->plan.tiles, c->stream), "relayout launch");
   HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   return FNNUE_OK;

@@ -305,6 +305,32 @@ __device__ __forceinline__ int sqr_crelu(int v) {
   return min(127, (int)(((unsigned)(a * a)) >> 19));
 }
 
+// Per-bucket weights as one wave holds them: the whole fc_0 matrix of a layer
+// stack as MFMA B fragments (HD/64 x 16 B per lane), plus fc_1/fc_2 pieces.
+template <int HD>
+struct StackRegs {
+  v4i w0[HD / 64];
+  v4i w1a, w1b;
+  int b0, b1a, b1b, w2a, w2b, b2;
+  __device__ __forceinline__ void load(const NetPtrs& net, int b, int r16, int g) {
+    const v4i* wr = reinterpret_cast<const v4i*>(net.w0 + ((size_t)b * kL2 + r16) * HD);
+#pragma unroll
+    for (int s = 0; s < HD / 64; ++s) w0[s] = wr[4 * s + g];
+    const int8_t* w1 = net.w1 + (size_t)b * kL3 * kFc1In;
+    w1a = g < 2 ? *reinterpret_cast<const v4i*>(w1 + r16 * kFc1In + 16 * g) : (v4i)0;
+    w1b = g < 2 ? *reinterpret_cast<const v4i*>(w1 + (16 + r16) * kFc1In + 16 * g) : (v4i)0;
+    b0 = net.b0[b * kL2 + r16];
+    b1a = net.b1[b * kL3 + r16];
+    b1b = net.b1[b * kL3 + 16 + r16];
+    w2a = net.w2[b * kL3 + r16];
+    w2b = net.w2[b * kL3 + 16 + r16];
+    b2 = net.b2[b];
+  }
+};
+
+// Persistent waves; wave w owns a contiguous range of 16-row tiles.  Rows come
+// bucket-sorted from the sliced FT (perm != null), so a wave's weights stay in
+// VGPRs across tiles and are reloaded only when the bucket changes.
 template <int HD>
 __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ bucket,
                                                     uint32_t n, NetPtrs net, int32_t* __restrict__ positional,
@@ -318,8 +344,12 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
   *reinterpret_cast<v4i*>(&x1s[wv][r16][16 * g]) = (v4i)0;
   wave_lds_sync();
   const uint32_t ntiles = (n + 15) / 16;
-  const uint32_t nw = gridDim.x * 4;
-  for (uint32_t tile = blockIdx.x * 4 + wv; tile < ntiles; tile += nw) {
+  const uint32_t nw = gridDim.x * 4, wid = blockIdx.x * 4 + wv;
+  const uint32_t per = (ntiles + nw - 1) / nw;
+  const uint32_t t_begin = wid * per, t_end = min(ntiles, t_begin + per);
+  StackRegs<HD> W;
+  int cur = -1;
+  for (uint32_t tile = t_begin; tile < t_end; ++tile) {
     const uint32_t p0 = tile * 16;
     const uint32_t prow = p0 + r16;
     const bool row_ok = prow < n;
@@ -336,15 +366,17 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
     while (bmask) {
       const int b = __builtin_ctz(bmask);
       bmask &= bmask - 1;
+      if (b != cur) {
+        W.load(net, b, r16, g);
+        cur = b;
+      }
       // fc_0: y[pos][out] = b0 + sum_k x[pos][k] * w0[out][k]
       v4i acc = (v4i)0;
-      const v4i* wr = reinterpret_cast<const v4i*>(net.w0 + ((size_t)b * kL2 + r16) * HD);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], wr[4 * s + g], acc, 0, 0, 0);
-      const int bias0 = net.b0[b * kL2 + r16];
+      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], W.w0[s], acc, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int y = acc[r] + bias0;
+        const int y = acc[r] + W.b0;
         const int p = 4 * g + r;
         if (r16 < kL2 - 1) {
           x1s[wv][p][r16] = (uint8_t)sqr_crelu(y);
@@ -357,26 +389,20 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
       wave_lds_sync();
       // fc_1 (30 -> 32, k padded to 64 with zeros), two MFMAs for outputs 0..15, 16..31.
       const v4i a1 = g < 2 ? *reinterpret_cast<const v4i*>(&x1s[wv][r16][16 * g]) : (v4i)0;
-      const int8_t* w1b = net.w1 + (size_t)b * kL3 * kFc1In;
-      const v4i wA = g < 2 ? *reinterpret_cast<const v4i*>(w1b + r16 * kFc1In + 16 * g) : (v4i)0;
-      const v4i wB = g < 2 ? *reinterpret_cast<const v4i*>(w1b + (16 + r16) * kFc1In + 16 * g) : (v4i)0;
-      const v4i z0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wA, (v4i)0, 0, 0, 0);
-      const v4i z1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, wB, (v4i)0, 0, 0, 0);
-      const int b1a = net.b1[b * kL3 + r16], b1b = net.b1[b * kL3 + 16 + r16];
-      const int w2a = net.w2[b * kL3 + r16], w2b = net.w2[b * kL3 + 16 + r16];
+      const v4i z0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, W.w1a, (v4i)0, 0, 0, 0);
+      const v4i z1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, W.w1b, (v4i)0, 0, 0, 0);
       int part[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) part[r] = w2a * crelu(z0[r] + b1a) + w2b * crelu(z1[r] + b1b);
+      for (int r = 0; r < 4; ++r) part[r] = W.w2a * crelu(z0[r] + W.b1a) + W.w2b * crelu(z1[r] + W.b1b);
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1)
 #pragma unroll
         for (int r = 0; r < 4; ++r) part[r] += __shfl_xor(part[r], o);
-      const int b2 = net.b2[b];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int p = 4 * g + r;
         const int pb = __shfl(bk, p);
-        if (r16 == 0 && pb == b) positional[perm ? perm[p0 + p] : p0 + p] = b2 + part[r] + fwds[wv][p];
+        if (r16 == 0 && pb == b) positional[perm ? perm[p0 + p] : p0 + p] = W.b2 + part[r] + fwds[wv][p];
       }
       wave_lds_sync();
     }
@@ -435,7 +461,7 @@ hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, c
                           const uint32_t* perm, hipStream_t stream) {
   const uint32_t tiles = (n + 15) / 16;
   uint32_t blocks = (tiles + 3) / 4;
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > 512) blocks = 512;  // persistent: 2 waves per SIMD resident, contiguous tile ranges
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional, perm);
   return hipGetLastError();

@@ -1,0 +1,82 @@
+"""Multi-GPU plumbing (one process per GPU, torch.distributed; backend "nccl"
+is RCCL over xGMI on MI355X, "gloo" is used for the CPU tests).
+
+The evaluation path shards without any data-path exchange: every rank
+evaluates its own positions.  The only collectives are:
+  * one broadcast of the packed net image from rank 0 (47 MB at HD = 1024),
+    which each rank then adopts with ``Evaluator(None, image_ptr=...)``;
+  * a max-reduction of the timed-region length (bench contract);
+  * an optional gather of per-rank results to rank 0 for a caller that wants
+    the whole batch in one place.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+
+def env_rank() -> tuple[int, int, int]:
+    """(rank, world_size, local_rank) from the torchrun environment."""
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
+        int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def shard_seed(seed: int, rank: int) -> int:
+    """Per-rank playout seed (weak scaling: every rank gets its own positions)."""
+    return seed + 1_000_003 * rank
+
+
+def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous [begin, end) share of `total` independent units (strong scaling)."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def broadcast_image(image: np.ndarray | None, device, src: int = 0):
+    """Broadcast rank `src`'s packed net image (uint8) to every rank.
+
+    Returns a uint8 tensor on `device` holding the image on every rank.
+    """
+    import torch
+    import torch.distributed as dist
+
+    rank = dist.get_rank()
+    if rank == src:
+        assert image is not None
+        buf = torch.from_numpy(np.ascontiguousarray(image, dtype=np.uint8)).to(device)
+        size = torch.tensor([buf.numel()], dtype=torch.int64, device=device)
+    else:
+        size = torch.zeros(1, dtype=torch.int64, device=device)
+    dist.broadcast(size, src)
+    if rank != src:
+        buf = torch.empty(int(size.item()), dtype=torch.uint8, device=device)
+    dist.broadcast(buf, src)
+    return buf
+
+
+def max_over_ranks(value: float, device) -> float:
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_to_rank0(local: np.ndarray, device):
+    """Concatenate every rank's 1-D int32 result array on rank 0 (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size()
+    n = torch.tensor([local.size], dtype=torch.int64, device=device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    cap = int(max(s.item() for s in sizes))
+    padded = torch.zeros(cap, dtype=torch.int32, device=device)
+    padded[: local.size] = torch.from_numpy(np.ascontiguousarray(local, dtype=np.int32)).to(device)
+    parts = [torch.zeros(cap, dtype=torch.int32, device=device) for _ in range(world)]
+    dist.all_gather(parts, padded)
+    if dist.get_rank() != 0:
+        return None
+    return np.concatenate([p[: int(s.item())].cpu().numpy() for p, s in zip(parts, sizes)])
