@@ -217,13 +217,18 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
   }
 }
 
+// Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
+// x 705 rows x 8 entries per row.  Single source of truth for the allocation
+// (sliced_tiles_bytes) and the relayout kernel's extent.
+__host__ __device__ constexpr size_t tile_uint4_count(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileRows * 8; }
+
 // ---------------------------------------------------------------------------
 // Tile image: tile(kb, s)[r][q] (16 B) = {ft_w[kb*704+r][32s+4q .. +3],
 // ft_w[kb*704+r][HD/2+32s+4q .. +3]}, r = 704 is the zero row.
 template <int HD>
 __global__ __launch_bounds__(256) void relayout_kernel(const int16_t* __restrict__ ftw, uint4* __restrict__ tiles) {
   constexpr int S = HD / 64;
-  const size_t total = (size_t)32 * S * kTileRows * 8;
+  constexpr size_t total = tile_uint4_count(HD);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int q = i & 7;
     const size_t t = i >> 3;
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const uint32_t word = e[2 * g + (t >> 1)];
-          const uint32_t r = (t & 1) ? (word >> 16) : (word & 0xFFFF);
+          const uint32_t r = min((t & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
           v[t] = img[r * 8 + q];
         }
 #pragma unroll
@@ -339,7 +344,7 @@ hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint
 
 }  // namespace
 
-size_t sliced_tiles_bytes(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileRows * 16; }
+size_t sliced_tiles_bytes(uint32_t hd) { return tile_uint4_count(hd) * sizeof(uint4); }
 size_t sliced_ctr_words() { return 3 * kBins + 16; }
 uint32_t sliced_max_units(uint32_t chunk) { return 32 + (2 * chunk + kUnitItems - 1) / kUnitItems; }
 
