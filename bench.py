@@ -2,14 +2,19 @@
 """Throughput bench: batched NNUE static evaluation on MI355X.
 
 Metric (BASELINE.json): NNUE positions evaluated/sec + % HBM roofline, bit-exact.
-Workload at N=1 = BASELINE config 2 (configs[1]): 1,000,000 random-playout
-positions (splitmix64 seed 1, L ~ U[0,160] random legal plies), synthetic
-SFNNv5 net with HD = 1024 (same shapes/format as nn-ad9b42354671.nnue, which
-is not available offline), accumulators from scratch.  A step = one
-fnnue_eval_positions_device call over the resident batch (feature
-transformer kernel + layer-stack kernel).  For N > 1 every rank evaluates its
-own 1M-position shard (weak scaling; positions are independent, no data-path
-collective); the net image is RCCL-broadcast from rank 0 once at start-up.
+
+Default workload (N=1 headline) = BASELINE config 2 (configs[1]): 1,000,000
+random-playout positions per GPU (splitmix64 seed 1, L ~ U[0,160] random legal
+plies), synthetic SFNNv5 net with HD = 1024 (same shapes and file format as
+nn-ad9b42354671.nnue, which is not available offline), accumulators from
+scratch.  A step = one fnnue_eval_*_device call over the HBM-resident batch.
+For N > 1 every rank evaluates its own shard (weak scaling; positions are
+independent, no data-path collective); the net image is RCCL-broadcast from
+rank 0 once at start-up.
+
+Other workloads (not the headline line; the other BASELINE configs, measured for DESIGN.md):
+  --workload games     config 3: random-playout games, every ply, incremental (CHAIN)
+  --workload children  config 4: every ply of random games plus all legal children (STAR)
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -29,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 METRIC = "NNUE positions evaluated/sec (1–8 MI355X) + % HBM roofline, bit-exact"
+PSQT_BUCKETS = 8
 
 
 def parse_args():
@@ -36,15 +42,44 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU")
+    ap.add_argument("--workload", choices=["positions", "games", "children"], default="positions")
+    ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions workload)")
+    ap.add_argument("--games", type=int, default=10_000, help="games per GPU (games / children workloads)")
     ap.add_argument("--hd", type=int, default=1024)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=0, help="host threads (0 = min(16, cpu_count))")
     ap.add_argument("--ft-impl", choices=["sliced", "gather"], default="sliced",
-                    help="feature-transformer kernel: LDS-stationary tiles (default) or per-position gather")
+                    help="feature-transformer kernel for independent positions")
     return ap.parse_args()
+
+
+def boards_of(pos: np.ndarray) -> np.ndarray:
+    b = np.zeros((len(pos), 64), dtype=np.uint8)
+    b[:, 0::2] = pos[:, :32] & 15
+    b[:, 1::2] = pos[:, :32] >> 4
+    return b
+
+
+def rows_scratch(board: np.ndarray) -> np.ndarray:
+    """Feature rows per position, both perspectives, from scratch (2n)."""
+    return 2 * (board != 0).sum(axis=1)
+
+
+def rows_incremental(board: np.ndarray, base: np.ndarray, has_base: np.ndarray) -> np.ndarray:
+    """Rows touched per position when derived from `base` (upstream update_accumulator):
+    per perspective, removed + added feature rows, or n rows on a refresh (no
+    base, that perspective's own king moved, or a diff larger than a refresh)."""
+    n = (board != 0).sum(axis=1)
+    changed = board != base
+    delta = ((base != 0) & changed).sum(axis=1) + ((board != 0) & changed).sum(axis=1)
+    rows = np.zeros(len(board), dtype=np.int64)
+    for king in (6, 14):
+        moved = (board == king).argmax(axis=1) != (base == king).argmax(axis=1)
+        refresh = ~has_base | moved | (2 * changed.sum(axis=1) >= n)
+        rows += np.where(refresh, n, delta)
+    return rows
 
 
 def main():
@@ -60,41 +95,68 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     threads = args.threads or min(16, os.cpu_count() or 1)
     torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     dist_on = world > 1
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=dev)
 
     # ---- net: synthesized on rank 0, device image broadcast over RCCL/xGMI ----
     t0 = time.time()
     image = F.Net.from_bytes(F.synthesize_net(args.seed, args.hd, 0)).image() if rank == 0 else None
-    if dist_on:
-        img = D.broadcast_image(image, torch.device("cuda", local))
-    else:
-        img = torch.from_numpy(image).cuda()
+    img = D.broadcast_image(image, dev) if dist_on else torch.from_numpy(image).to(dev)
     torch.cuda.synchronize()
     ev = F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=args.hd)
     ev.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
     del img
     t_net = time.time() - t0
 
-    # ---- inputs: this rank's shard of random-playout positions, resident in HBM ----
+    # ---- inputs: this rank's shard, resident in HBM ----
     t0 = time.time()
-    pos = F.random_playouts(D.shard_seed(args.seed, rank), args.positions, 0, 160, threads=threads)
+    seed = D.shard_seed(args.seed, rank)
+    off = None
+    if args.workload == "positions":
+        pos = F.random_playouts(seed, args.positions, 0, 160, threads=threads)
+        board = boards_of(pos)
+        rows = rows_scratch(board)
+        workload = ("BASELINE config 2: random-playout positions (splitmix64, L~U[0,160]), from-scratch "
+                    "accumulators, synthetic SFNNv5 net (HalfKAv2_hm, HD=%d)" % args.hd)
+    else:
+        mode = F.PLAYOUT_PLIES if args.workload == "games" else F.PLAYOUT_CHILDREN
+        pos, off = F.random_playouts(seed + 1, args.games, 0, 160, mode=mode, threads=threads)
+        board = boards_of(pos)
+        starts = off[:-1].astype(np.int64)
+        has_base = np.ones(len(pos), dtype=bool)
+        has_base[starts] = False
+        if args.workload == "games":
+            base_idx = np.arange(len(pos)) - 1
+        else:
+            base_idx = starts[np.repeat(np.arange(len(starts)), np.diff(off))]
+        base_idx[~has_base] = 0
+        rows = rows_incremental(board, board[base_idx], has_base)
+        workload = ("BASELINE config %s: %d random-playout games per GPU, %s, synthetic SFNNv5 net (HD=%d)"
+                    % ("3" if args.workload == "games" else "4", args.games,
+                       "every ply, incremental CHAIN" if args.workload == "games"
+                       else "every ply + all legal 1-ply children, STAR", args.hd))
     t_gen = time.time() - t0
-    board = np.zeros((len(pos), 64), dtype=np.uint8)
-    board[:, 0::2] = pos[:, :32] & 15
-    board[:, 1::2] = pos[:, :32] >> 4
+    npos = len(pos)
     pieces = (board != 0).sum(axis=1)
-    mean_n = float(pieces.mean())
-    d_pos = torch.from_numpy(pos).cuda()
-    d_psqt = torch.zeros(len(pos), dtype=torch.int32, device="cuda")
-    d_positional = torch.zeros(len(pos), dtype=torch.int32, device="cuda")
+    d_pos = torch.from_numpy(pos).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int32)).to(dev) if off is not None else None
+    d_psqt = torch.zeros(npos, dtype=torch.int32, device=dev)
+    d_positional = torch.zeros(npos, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
 
-    def step():
-        ev.eval_positions_device(d_pos.data_ptr(), len(pos), d_psqt.data_ptr(), d_positional.data_ptr(),
-                                 stream.cuda_stream)
+    if off is None:
+        def step():
+            ev.eval_positions_device(d_pos.data_ptr(), npos, d_psqt.data_ptr(), d_positional.data_ptr(),
+                                     stream.cuda_stream)
+    else:
+        gmode = F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR
+
+        def step():
+            ev.eval_groups_device(d_pos.data_ptr(), d_off.data_ptr(), len(off) - 1, npos, gmode,
+                                  d_psqt.data_ptr(), d_positional.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -115,33 +177,36 @@ def main():
     launches, ft_ms, stack_ms = ev.timing_read()
     ev.set_timing(False)
     ev.check()
-
-    elapsed_max = D.max_over_ranks(elapsed, torch.device("cuda", local)) if dist_on else elapsed
-    total_positions = args.positions * world * args.steps
-    value = total_positions / elapsed_max
+    if dist_on:
+        elapsed_max = D.max_over_ranks(elapsed, dev)
+        tot = torch.tensor([float(npos)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        total_positions = float(tot.item())
+    else:
+        elapsed_max, total_positions = elapsed, float(npos)
+    value = total_positions * args.steps / elapsed_max
 
     # ---- roofline of the dominant kernel (feature transformer) ----
-    # algorithmic bytes/position = n * (2*HD*2 + 4*PB*2) + 36 in + 8 out.
-    per_pos = pieces.astype(np.float64) * (2 * args.hd * 2 + 2 * 4 * 8) + 36 + 8
-    bytes_per_launch = float(per_pos.sum())
+    # each feature row costs 2*HD bytes of FT weights + 4*PB bytes of PSQT
+    # weights; + 36 B position in + 8 B results out.
+    bytes_per_launch = float(rows.sum()) * (2 * args.hd + 4 * PSQT_BUCKETS) + npos * (36 + 8)
     ft_avg_ms = ft_ms / max(launches, 1)
     stack_avg_ms = stack_ms / max(launches, 1)
     achieved_gbs = bytes_per_launch / (ft_avg_ms * 1e-3) / 1e9
 
-    # ---- results back to host (outside the timed region): spot parity + CPU baseline ----
+    # ---- results back to host (outside the timed region): parity spot check + CPU baseline ----
     psqt = d_psqt.cpu().numpy()
     positional = d_positional.cpu().numpy()
     cpu = None
     parity = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import OracleNet  # cpu_baseline leg: the oracle is the timed CPU port
         on = OracleNet(F.synthesize_net(args.seed, args.hd, 0))
-        done, t0 = 0, time.perf_counter()
+        done, mism, t0 = 0, 0, time.perf_counter()
         chunk = 100_000
-        mism = 0
         while True:
-            lo = done % len(pos)
-            hi = min(lo + chunk, len(pos))
+            lo = done % npos
+            hi = min(lo + chunk, npos)
             ps, po, rc = on.eval_packed(pos[lo:hi], threads=threads)
             assert rc == 0
             mism += int(((ps != psqt[lo:hi]) | (po != positional[lo:hi])).sum())
@@ -150,9 +215,9 @@ def main():
                 break
         cpu_el = time.perf_counter() - t0
         cpu = {"value": done / cpu_el, "unit": "positions/s", "cores": threads, "kind": "port",
-               "sample": f"{done} positions of the same workload (first {min(done, len(pos))} of the batch, "
-                         f"{cpu_el:.1f} s wall on {threads} threads, scalar C oracle -O3 -march=x86-64-v3)"}
-        parity = {"checked": min(done, len(pos)), "mismatches": mism}
+               "sample": f"{done} positions of the same workload (from-scratch refresh per position, "
+                         f"{cpu_el:.1f} s wall on {threads} threads; oracle/nnue_oracle.c -O3 -march=x86-64-v3)"}
+        parity = {"checked": min(done, npos), "mismatches": mism}
 
     if rank == 0:
         out = {
@@ -169,13 +234,12 @@ def main():
             "dtype": "int16",
             "data": "synthetic",
             "config": {
-                "workload": "BASELINE config 2: random-playout positions (splitmix64, L~U[0,160]), "
-                            "from-scratch accumulators, synthetic SFNNv5 net (HalfKAv2_hm, HD=%d)" % args.hd,
-                "positions_per_gpu": args.positions,
-                "mean_pieces": round(mean_n, 3),
+                "workload": workload,
+                "positions_per_gpu": npos,
+                "mean_pieces": round(float(pieces.mean()), 3),
                 "hd": args.hd,
                 "parallelism": f"dp{world}",
-                "ft_impl": args.ft_impl,
+                "ft_impl": args.ft_impl if off is None else "groups",
             },
             "roofline": {
                 "bound": "hbm",
@@ -184,15 +248,15 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": None,
-                "kernel": "feature transformer (%s)" % ("ft_slices_kernel + plan_*" if args.ft_impl == "sliced"
-                                                         else "ft_scratch_kernel"),
+                "kernel": ("ft_slices_kernel + plan_* (LDS-stationary FT)" if off is None and args.ft_impl == "sliced"
+                           else "ft_scratch_kernel" if off is None else "ft_groups_kernel"),
                 "kernel_avg_ms": round(ft_avg_ms, 4),
                 "stack_kernel_avg_ms": round(stack_avg_ms, 4),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
             },
             "cpu_baseline": cpu,
             "parity_spot_check": parity,
-            "setup_s": {"net": round(t_net, 2), "playouts": round(t_gen, 2)},
+            "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
         print(json.dumps(out), flush=True)
     ev.close()

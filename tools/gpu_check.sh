@@ -16,7 +16,10 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_gather) run bench_gather 600 python bench.py --ft-impl gather --no-cpu-baseline ;;
+    bench_games) run bench_games 600 python bench.py --workload games --no-cpu-baseline ;;
+    bench_children) run bench_children 600 python bench.py --workload children --games 1000 --no-cpu-baseline ;;
     profile) run profile 1200 tools/profile.sh "${PROFILE_TAG:-rXX}" ;;
+    profile_gather) run profile_gather 1200 tools/profile.sh "${PROFILE_TAG:-rXX}_gather" --ft-impl gather ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

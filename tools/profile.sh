@@ -1,16 +1,19 @@
 #!/bin/bash
-# rocprofv3 evidence for the bench workload (run on the GPU box from the repo root):
+# rocprofv3 evidence for a bench workload (run on the GPU box from the repo root):
 #   kernel trace + stats, then one PMC pass per counter group (never combined
 #   with tracing domains).  Outputs under gpurun_out/prof_<tag>/.
+#   usage: tools/profile.sh <tag> [extra bench.py args...]
 set -euo pipefail
-TAG=${1:-r01}
+TAG=${1:-rXX}; shift || true
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS="--steps ${STEPS:-10} --warmup 2 --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+  python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > "$OUT/trace.log" 2>&1
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
   name=$(echo "$pmc" | tr ' ' '_')
-  timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc_$name" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$name.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc_$name" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$OUT/pmc_$name.log" 2>&1
 done
+python3 tools/pmc_summary.py "$OUT" > "$OUT/pmc_summary.txt"
 echo "profile done: $OUT"
