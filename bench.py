@@ -70,15 +70,15 @@ def rows_scratch(board: np.ndarray) -> np.ndarray:
 def rows_incremental(board: np.ndarray, base: np.ndarray, has_base: np.ndarray) -> np.ndarray:
     """Rows touched per position when derived from `base` (upstream update_accumulator):
     per perspective, removed + added feature rows, or n rows on a refresh (no
-    base, that perspective's own king moved, or a diff larger than a refresh)."""
+    base, or that perspective's own king moved); never more than a refresh."""
     n = (board != 0).sum(axis=1)
     changed = board != base
     delta = ((base != 0) & changed).sum(axis=1) + ((board != 0) & changed).sum(axis=1)
     rows = np.zeros(len(board), dtype=np.int64)
     for king in (6, 14):
         moved = (board == king).argmax(axis=1) != (base == king).argmax(axis=1)
-        refresh = ~has_base | moved | (2 * changed.sum(axis=1) >= n)
-        rows += np.where(refresh, n, delta)
+        refresh = ~has_base | moved
+        rows += np.where(refresh, n, np.minimum(n, delta))
     return rows
 
 
@@ -219,6 +219,16 @@ def main():
                          f"{cpu_el:.1f} s wall on {threads} threads; oracle/nnue_oracle.c -O3 -march=x86-64-v3)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
 
+    # roofline.traffic: PMC-measured bytes per launch of the same workload, from the
+    # committed profile (tools/profile.sh + tools/traffic.py -> profiles/traffic.json).
+    traffic, traffic_src = None, None
+    tkey = f"{args.workload}:{args.ft_impl if off is None else 'groups'}:hd{args.hd}"
+    tpath = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(tpath):
+        entry = json.load(open(tpath)).get(tkey)
+        if entry:
+            traffic, traffic_src = entry["bytes_per_launch"], entry["source"]
+
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -247,7 +257,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": ("ft_slices_kernel + plan_* (LDS-stationary FT)" if off is None and args.ft_impl == "sliced"
                            else "ft_scratch_kernel" if off is None else "ft_groups_kernel"),
                 "kernel_avg_ms": round(ft_avg_ms, 4),

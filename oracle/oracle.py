@@ -101,7 +101,7 @@ class OracleNet:
         return b, x, y, acc
 
     def __del__(self):
-        if getattr(self, "_h", None) and self._h.value:
+        if getattr(self, "_h", None) and self._h.value and lib is not None:
             lib.oracle_net_free(self._h)
             self._h = C.c_void_p()
 
