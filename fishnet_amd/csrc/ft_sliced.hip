@@ -39,7 +39,7 @@ constexpr int kNoRow = kRowsPerBlock;         // padding entry -> zero row
 constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
 constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
 constexpr int kBins = kItemBins + kPosBins;
-constexpr int kScatterPositions = 512;        // positions per plan_scatter workgroup
+constexpr int kScatterPositions = 256;        // positions per plan_scatter workgroup (one per lane)
 
 // Counter block layout (uint32 words).
 constexpr int kCnt = 0, kOff = kBins, kCur = 2 * kBins, kNUnits = 3 * kBins;
@@ -59,26 +59,81 @@ __device__ __forceinline__ void lane_item(int lane, int& item, int& q) {
 }
 
 // ---------------------------------------------------------------------------
+// Lane-per-position decode of a packed position (64 nibbles in 8 words) with
+// SWAR nibble tests: the plan kernels touch every position once, so they
+// decode 64 positions per wave instead of one.
+struct LaneBoard {
+  uint32_t w[8];
+  uint64_t occ;
+  int stm, wk, bk, cnt;
+  bool ok;
+};
+
+// Bit 4k+3 set iff nibble k of y is zero.
+__device__ __forceinline__ uint32_t zero_nibbles(uint32_t y) {
+  return ~(((y & 0x77777777u) + 0x77777777u) | y) & 0x88888888u;
+}
+
+// Compresses bits 3, 7, ..., 31 into an 8-bit mask.
+__device__ __forceinline__ uint32_t nibble_bits(uint32_t z) {
+  uint32_t m = z >> 3;
+  m = (m | (m >> 3)) & 0x03030303u;
+  m = (m | (m >> 6)) & 0x000F000Fu;
+  return (m | (m >> 12)) & 0xFFu;
+}
+
+__device__ __forceinline__ LaneBoard lane_decode(const fnnue_pos* p) {
+  LaneBoard b;
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b.w[i] = pw[i];
+  b.stm = (int)(pw[8] & 0xFF);
+  b.occ = 0;
+  int nwk = 0, nbk = 0;
+  uint32_t bad = 0;
+  b.wk = b.bk = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = b.w[i];
+    b.occ |= (uint64_t)nibble_bits(~zero_nibbles(w) & 0x88888888u) << (8 * i);
+    const uint32_t kw = zero_nibbles(w ^ 0x66666666u), kb = zero_nibbles(w ^ 0xEEEEEEEEu);
+    nwk += __popc(kw);
+    nbk += __popc(kb);
+    if (kw) b.wk = 8 * i + (__builtin_ctz(kw) >> 2);
+    if (kb) b.bk = 8 * i + (__builtin_ctz(kb) >> 2);
+    bad |= zero_nibbles(w ^ 0x77777777u) | zero_nibbles(w ^ 0x88888888u) | zero_nibbles(~w);
+  }
+  b.cnt = __popcll(b.occ);
+  b.ok = !bad && nwk == 1 && nbk == 1 && b.cnt <= 32 && b.stm <= 1;
+  return b;
+}
+
+__device__ __forceinline__ int nibble_at(const uint32_t (&w)[8], int s) {
+  const int i = s >> 3;
+  const uint32_t a = (i & 1) ? w[1] : w[0], c = (i & 1) ? w[3] : w[2];
+  const uint32_t e = (i & 1) ? w[5] : w[4], g = (i & 1) ? w[7] : w[6];
+  const uint32_t lo = (i & 2) ? c : a, hi = (i & 2) ? g : e;
+  return (int)((((i & 4) ? hi : lo) >> (4 * (s & 7))) & 15u);
+}
+
 __global__ __launch_bounds__(256) void plan_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
                                                          uint32_t* __restrict__ ctr, uint32_t* __restrict__ err) {
   __shared__ uint32_t h[kBins];
   for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < n; p += nw) {
-    const Decoded d = decode(pos + p, lane);
-    if (lane == 0) {
-      if (!d.ok) {
-        atomicOr(err, 1u);
-        atomicAdd(&h[kItemBins + 8], 1u);
-      } else {
-        atomicAdd(&h[king_block(0, d.wk) * 33 + d.cnt], 1u);
-        atomicAdd(&h[king_block(1, d.bk) * 33 + d.cnt], 1u);
-        atomicAdd(&h[kItemBins + ((d.cnt - 1) >> 2)], 1u);
-      }
+  uint32_t bad = 0;
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+    const LaneBoard b = lane_decode(pos + p);
+    if (!b.ok) {
+      bad = 1;
+      atomicAdd(&h[kItemBins + 8], 1u);
+    } else {
+      atomicAdd(&h[king_block(0, b.wk) * 33 + b.cnt], 1u);
+      atomicAdd(&h[king_block(1, b.bk) * 33 + b.cnt], 1u);
+      atomicAdd(&h[kItemBins + ((b.cnt - 1) >> 2)], 1u);
     }
   }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(err, 1u);
   __syncthreads();
   for (int i = threadIdx.x; i < kBins; i += blockDim.x)
     if (h[i]) atomicAdd(&ctr[kCnt + i], h[i]);
@@ -138,6 +193,8 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
 }
 
 // Item record: (n << 24) | (slot << 1) | half, half 0 = side-to-move half of x.
+// One lane per position; the workgroup's 256 positions get local ranks from
+// LDS atomics, then reserve one range per bin with a single global atomic.
 __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
                                                            const int32_t* __restrict__ psqw,
                                                            uint32_t* __restrict__ ctr, uint32_t* __restrict__ items,
@@ -146,75 +203,75 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
                                                            int32_t* __restrict__ psqt_out) {
   __shared__ uint32_t lcnt[kBins];
   __shared__ uint32_t lbase[kBins];
-  __shared__ uint16_t rank[3][kScatterPositions];
-  __shared__ uint16_t rows[4][2][64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t p0 = blockIdx.x * kScatterPositions;
-  const uint32_t pend = min(n, p0 + kScatterPositions);
   for (int i = threadIdx.x; i < kBins; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
-  // Pass A: local ranks.
-  for (uint32_t p = p0 + wv; p < pend; p += 4) {
-    const Decoded d = decode(pos + p, lane);
-    if (lane == 0) {
-      const uint32_t lp = p - p0;
-      if (d.ok) {
-        rank[0][lp] = (uint16_t)atomicAdd(&lcnt[king_block(0, d.wk) * 33 + d.cnt], 1u);
-        rank[1][lp] = (uint16_t)atomicAdd(&lcnt[king_block(1, d.bk) * 33 + d.cnt], 1u);
-        rank[2][lp] = (uint16_t)atomicAdd(&lcnt[kItemBins + ((d.cnt - 1) >> 2)], 1u);
-      } else {
-        rank[2][lp] = (uint16_t)atomicAdd(&lcnt[kItemBins + 8], 1u);
-      }
+  const uint32_t p = blockIdx.x * kScatterPositions + threadIdx.x;
+  const bool live = p < n;
+  LaneBoard b;
+  int kw = 0, kb = 0, kp = kItemBins + 8;
+  uint32_t rw = 0, rb = 0, rp = 0;
+  if (live) {
+    b = lane_decode(pos + p);
+    if (b.ok) {
+      kw = king_block(0, b.wk) * 33 + b.cnt;
+      kb = king_block(1, b.bk) * 33 + b.cnt;
+      kp = kItemBins + ((b.cnt - 1) >> 2);
+      rw = atomicAdd(&lcnt[kw], 1u);
+      rb = atomicAdd(&lcnt[kb], 1u);
     }
+    rp = atomicAdd(&lcnt[kp], 1u);
   }
   __syncthreads();
-  // Reserve this workgroup's range in every bin it uses.
   for (int i = threadIdx.x; i < kBins; i += blockDim.x)
     lbase[i] = lcnt[i] ? atomicAdd(&ctr[kCur + i], lcnt[i]) : 0;
   __syncthreads();
-  // Pass B: scatter.
-  for (uint32_t p = p0 + wv; p < pend; p += 4) {
-    const Decoded d = decode(pos + p, lane);
-    const uint32_t lp = p - p0;
-    if (!d.ok) {
-      if (lane == 0) {
-        const uint32_t slot = lbase[kItemBins + 8] + rank[2][lp];
-        perm[slot] = p;
-        bucket_out[slot] = 0xFF;
-        psqt_out[p] = 0;
-      }
-      continue;
+  if (!live) return;
+  const uint32_t slot = lbase[kp] + rp;
+  perm[slot] = p;
+  if (!b.ok) {
+    bucket_out[slot] = 0xFF;
+    psqt_out[p] = 0;
+    return;
+  }
+  const int bucket = (b.cnt - 1) >> 2;
+  const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
+  const int kbw = king_block(0, b.wk), kbb = king_block(1, b.bk);
+  uint32_t ew[16], eb[16];
+  uint32_t pw = 0, pb = 0;
+  uint64_t m = b.occ;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t a = kNoRow, c = kNoRow;
+    if (m) {
+      const int sq = __builtin_ctzll(m);
+      m &= m - 1;
+      const int pc = nibble_at(b.w, sq);
+      const int fw = make_index(0, sq, pc, b.wk), fb = make_index(1, sq, pc, b.bk);
+      a = (uint32_t)(fw - kRowsPerBlock * kbw);
+      c = (uint32_t)(fb - kRowsPerBlock * kbb);
+      pw += (uint32_t)psqw[fw * kPsqtBuckets + bucket];
+      pb += (uint32_t)psqw[fb * kPsqtBuckets + bucket];
     }
-    const int bucket = (d.cnt - 1) >> 2;
-    const uint32_t slot = lbase[kItemBins + bucket] + rank[2][lp];
-    const int kbw = king_block(0, d.wk), kbb = king_block(1, d.bk);
-    const uint32_t iw = lbase[kbw * 33 + d.cnt] + rank[0][lp];
-    const uint32_t ib = lbase[kbb * 33 + d.cnt] + rank[1][lp];
-    int fw = kZeroRow, fb = kZeroRow;
-    if (d.pc) {
-      fw = make_index(0, lane, d.pc, d.wk);
-      fb = make_index(1, lane, d.pc, d.bk);
-      // compact the rows (relative to the king block) in square order
-      const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(d.occ >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)d.occ, 0));
-      rows[wv][0][r] = (uint16_t)(fw - kRowsPerBlock * kbw);
-      rows[wv][1][r] = (uint16_t)(fb - kRowsPerBlock * kbb);
-    }
-    const int v = psqw[fw * kPsqtBuckets + bucket] - psqw[fb * kPsqtBuckets + bucket];
-    int tot = wave_sum(v);
-    if (d.stm) tot = -tot;
-    wave_lds_sync();
-    const int persp = lane >> 5, k = lane & 31;
-    const uint16_t e = k < d.cnt ? rows[wv][persp][k] : (uint16_t)kNoRow;
-    flist[(size_t)(persp ? ib : iw) * 32 + k] = e;
-    wave_lds_sync();
-    if (lane == 0) {
-      items[iw] = ((uint32_t)d.cnt << 24) | (slot << 1) | (uint32_t)(d.stm != 0);
-      items[ib] = ((uint32_t)d.cnt << 24) | (slot << 1) | (uint32_t)(d.stm != 1);
-      perm[slot] = p;
-      bucket_out[slot] = (uint8_t)bucket;
-      psqt_out[p] = tot / 2;
+    if (k & 1) {
+      ew[k >> 1] |= a << 16;
+      eb[k >> 1] |= c << 16;
+    } else {
+      ew[k >> 1] = a;
+      eb[k >> 1] = c;
     }
   }
+  uint4* fw4 = reinterpret_cast<uint4*>(flist + (size_t)iw * 32);
+  uint4* fb4 = reinterpret_cast<uint4*>(flist + (size_t)ib * 32);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fw4[k] = make_uint4(ew[4 * k], ew[4 * k + 1], ew[4 * k + 2], ew[4 * k + 3]);
+    fb4[k] = make_uint4(eb[4 * k], eb[4 * k + 1], eb[4 * k + 2], eb[4 * k + 3]);
+  }
+  items[iw] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 0);
+  items[ib] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 1);
+  bucket_out[slot] = (uint8_t)bucket;
+  // psqt = (psqtAcc[stm][bucket] - psqtAcc[~stm][bucket]) / 2, int32 wrap then C division
+  psqt_out[p] = (int32_t)(b.stm ? pb - pw : pw - pb) / 2;
 }
 
 // Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
@@ -257,7 +314,28 @@ __device__ __forceinline__ uint32_t transform4(u16x4 lo, u16x4 hi) {
   return (uint32_t)pr.x | ((uint32_t)pr.y << 8) | ((uint32_t)pr.z << 16) | ((uint32_t)pr.w << 24);
 }
 
-// One workgroup = one (unit, slice).  16 waves x 8 items per pass.
+// Loads one pass's item record and its 32 feature rows (16 dwords, two u16
+// each).  The index is clamped into the unit so the loads are unconditional
+// (no exec branch around them: hipcc then counts vmcnt instead of draining it).
+__device__ __forceinline__ void load_pass(const uint32_t* __restrict__ items, const uint16_t* __restrict__ flist,
+                                          int it, uint32_t& rec, uint32_t (&e)[16]) {
+  rec = items[it];
+  const uint4* fl = reinterpret_cast<const uint4*>(flist + (size_t)it * 32);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint4 v = fl[k];
+    e[4 * k] = v.x;
+    e[4 * k + 1] = v.y;
+    e[4 * k + 2] = v.z;
+    e[4 * k + 3] = v.w;
+  }
+}
+
+// One workgroup = one (unit, slice).  16 waves x 8 items per pass; the next
+// pass's records and feature lists are prefetched into registers while the
+// current pass reads the LDS tile.  Items of a unit are sorted by piece count,
+// so a pass's longest list is that of its item 7 (clamped into the unit),
+// whose record lane 48 holds (lane_item).
 template <int HD>
 __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict__ tiles,
                                                          const int16_t* __restrict__ ftb,
@@ -267,6 +345,8 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          const uint16_t* __restrict__ flist,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
+  constexpr int kRowsPerGroup = 8;
+  constexpr int kLastItemLane = 48;
   __shared__ uint4 img[kTileRows * 8];
   const uint32_t w = blockIdx.x;
   const uint32_t j = w >> 3;
@@ -276,54 +356,46 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   const int4 u = units[unit];
   const uint4* src = tiles + ((size_t)u.x * S + s) * kTileRows * 8;
   for (int i = threadIdx.x; i < kTileRows * 8; i += 1024) img[i] = src[i];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;
   lane_item(lane, it_in_wave, q);
   const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
   const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+  int base = u.y + wv * 8;
+  uint32_t rec, e[16];
+  load_pass(items, flist, min(base + it_in_wave, u.z - 1), rec, e);
   __syncthreads();
-  for (int base = u.y + wv * 8; base < u.z; base += 16 * 8) {
-    const int it = base + it_in_wave;
-    const bool valid = it < u.z;
-    const uint32_t rec = valid ? items[it] : 0;
-    const int ni = (int)(rec >> 24);
-    int maxn = ni;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) maxn = max(maxn, __shfl_xor(maxn, o));
-    uint32_t e[16];
-    if (valid) {
-      const uint4* fl = reinterpret_cast<const uint4*>(flist + (size_t)it * 32);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint4 v = fl[k];
-        e[4 * k] = v.x; e[4 * k + 1] = v.y; e[4 * k + 2] = v.z; e[4 * k + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) e[k] = (uint32_t)kNoRow * 0x10001u;
-    }
+  int maxn = (int)(__builtin_amdgcn_readlane(rec, kLastItemLane) >> 24);
+  for (; base < u.z; base += 16 * 8) {
+    uint32_t nrec, ne[16];
+    load_pass(items, flist, min(base + 16 * 8 + it_in_wave, u.z - 1), nrec, ne);
     u16x4 lo = b_lo, hi = b_hi;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      if (4 * g < maxn) {
-        uint4 v[4];
+    for (int g = 0; g < 32 / kRowsPerGroup; ++g) {
+      if (kRowsPerGroup * g < maxn) {
+        uint4 v[kRowsPerGroup];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const uint32_t word = e[2 * g + (t >> 1)];
+        for (int t = 0; t < kRowsPerGroup; ++t) {
+          const uint32_t word = e[(kRowsPerGroup * g + t) >> 1];
           const uint32_t r = min((t & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
           v[t] = img[r * 8 + q];
         }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < kRowsPerGroup; ++t) {
           lo += __builtin_bit_cast(u16x4, make_uint2(v[t].x, v[t].y));
           hi += __builtin_bit_cast(u16x4, make_uint2(v[t].z, v[t].w));
         }
       }
     }
-    if (valid) {
+    if (base + it_in_wave < u.z) {
       const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
       *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
     }
+    rec = nrec;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) e[k] = ne[k];
+    maxn = (int)(__builtin_amdgcn_readlane(rec, kLastItemLane) >> 24);
   }
 }
 
@@ -369,8 +441,7 @@ hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const
   if (n == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
-  const uint32_t waves = n;
-  uint32_t blocks = (waves + 3) / 4;
+  uint32_t blocks = (n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(plan_count_kernel, dim3(blocks), dim3(256), 0, stream, pos, n, P.ctr, err);
   if ((e = hipGetLastError()) != hipSuccess) return e;

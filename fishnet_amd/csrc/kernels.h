@@ -37,7 +37,7 @@ hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, ui
                         int32_t* positional, const uint32_t* perm, hipStream_t stream);
 
 // LDS-stationary feature transformer (ft_sliced.hip).
-constexpr uint32_t kUnitItems = 2048;  // perspective-items per (king block) work unit
+constexpr uint32_t kUnitItems = 4096;  // perspective-items per (king block) work unit
 struct SlicedPlan {
   void* tiles;       // [32 king blocks][hd/64 slices][705 rows][8] x 16 B (relayout of ft_w)
   uint32_t* ctr;     // sliced_ctr_words() counters / offsets
