@@ -97,7 +97,8 @@ void ctx_destroy(fnnue_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off,
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
-                  (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm})
+                  (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm,
+                  (void*)c->plan.psqt_part})
     if (p) (void)hipFree(p);
   delete c;
 }
@@ -142,7 +143,8 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
       hipMalloc(&P.units, (size_t)sliced_max_units(kChunk) * 16) != hipSuccess ||
       hipMalloc(&P.items, (size_t)2 * kChunk * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&P.flist, (size_t)2 * kChunk * 32 * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&P.perm, (size_t)kChunk * sizeof(uint32_t)) != hipSuccess)
+      hipMalloc(&P.perm, (size_t)kChunk * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.psqt_part, (size_t)2 * kChunk * sizeof(int32_t)) != hipSuccess)
     return fail(FNNUE_E_OOM, "device allocation (sliced plan)");
   if (const char* impl = std::getenv("FNNUE_FT_IMPL"))
     c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
@@ -226,9 +228,10 @@ int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
 
 // Runs the stack kernel for [0, n) of the workspace and records timing.
 int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 3>* ev,
-                   const uint32_t* perm = nullptr) {
+                   const uint32_t* perm = nullptr, const int32_t* psqt_part = nullptr, int32_t* d_psqt = nullptr) {
   if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
-  HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, perm, s), "stack kernel launch");
+  HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, perm, psqt_part, d_psqt, s),
+          "stack kernel launch");
   if (ev) HIP_TRY(hipEventRecord((*ev)[2], s), "hipEventRecord");
   return FNNUE_OK;
 }
@@ -423,6 +426,7 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
     if (rc) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
     const uint32_t* perm = nullptr;
+    const int32_t* psqt_part = nullptr;
     if (ctx->ft_impl == FNNUE_FT_GATHER) {
       HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_scratch launch");
@@ -431,8 +435,9 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
                                ctx->err, s),
               "ft_sliced launch");
       perm = ctx->plan.perm;
+      psqt_part = ctx->plan.psqt_part;
     }
-    rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, perm);
+    rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, perm, psqt_part, d_psqt + b);
     if (rc) return rc;
   }
   return FNNUE_OK;

@@ -196,7 +196,6 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
 // One lane per position; the workgroup's 256 positions get local ranks from
 // LDS atomics, then reserve one range per bin with a single global atomic.
 __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                                           const int32_t* __restrict__ psqw,
                                                            uint32_t* __restrict__ ctr, uint32_t* __restrict__ items,
                                                            uint16_t* __restrict__ flist, uint32_t* __restrict__ perm,
                                                            uint8_t* __restrict__ bucket_out,
@@ -237,7 +236,6 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
   const int kbw = king_block(0, b.wk), kbb = king_block(1, b.bk);
   uint32_t ew[16], eb[16];
-  uint32_t pw = 0, pb = 0;
   uint64_t m = b.occ;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
@@ -249,8 +247,6 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
       const int fw = make_index(0, sq, pc, b.wk), fb = make_index(1, sq, pc, b.bk);
       a = (uint32_t)(fw - kRowsPerBlock * kbw);
       c = (uint32_t)(fb - kRowsPerBlock * kbb);
-      pw += (uint32_t)psqw[fw * kPsqtBuckets + bucket];
-      pb += (uint32_t)psqw[fb * kPsqtBuckets + bucket];
     }
     if (k & 1) {
       ew[k >> 1] |= a << 16;
@@ -270,8 +266,7 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
   items[iw] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;
-  // psqt = (psqtAcc[stm][bucket] - psqtAcc[~stm][bucket]) / 2, int32 wrap then C division
-  psqt_out[p] = (int32_t)(b.stm ? pb - pw : pw - pb) / 2;
+  // the PSQT term is summed from LDS by the slice-0 workgroups of ft_slices
 }
 
 // Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
@@ -343,11 +338,14 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          const int4* __restrict__ units,
                                                          const uint32_t* __restrict__ items,
                                                          const uint16_t* __restrict__ flist,
+                                                         const int32_t* __restrict__ psqw,
+                                                         int32_t* __restrict__ psqt_part,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
   constexpr int kRowsPerGroup = 8;
   constexpr int kLastItemLane = 48;
   __shared__ uint4 img[kTileRows * 8];
+  __shared__ int32_t ptile[kTileRows * kPsqtBuckets];  // slice 0 only: PSQT rows of the king block
   const uint32_t w = blockIdx.x;
   const uint32_t j = w >> 3;
   const uint32_t unit = (j / S) * 8 + (w & 7);
@@ -356,6 +354,11 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   const int4 u = units[unit];
   const uint4* src = tiles + ((size_t)u.x * S + s) * kTileRows * 8;
   for (int i = threadIdx.x; i < kTileRows * 8; i += 1024) img[i] = src[i];
+  if (s == 0) {
+    const int32_t* psrc = psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets;
+    for (int i = threadIdx.x; i < kTileRows * kPsqtBuckets; i += 1024)
+      ptile[i] = i < kRowsPerBlock * kPsqtBuckets ? psrc[i] : 0;
+  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;
@@ -388,9 +391,25 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
         }
       }
     }
-    if (base + it_in_wave < u.z) {
+    const bool valid = base + it_in_wave < u.z;
+    if (valid) {
       const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
       *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
+    }
+    if (s == 0) {
+      // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32 wrap).
+      const int ni = (int)(rec >> 24);
+      const int bucket = (max(ni, 1) - 1) >> 2;
+      uint32_t acc = 0;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        if (k < maxn) {
+          const uint32_t word = e[k >> 1];
+          const uint32_t r = min((k & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
+          acc += (uint32_t)ptile[r * kPsqtBuckets + bucket];
+        }
+      }
+      if (valid && q == 0) psqt_part[((rec >> 1) & 0x7FFFFF) * 2 + (rec & 1)] = (int32_t)acc;
     }
     rec = nrec;
 #pragma unroll
@@ -410,7 +429,8 @@ hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint
   constexpr int S = HD / 64;
   const uint32_t groups = (max_units + 7) / 8;
   hipLaunchKernelGGL((ft_slices_kernel<HD>), dim3(groups * 8 * S), dim3(1024), 0, stream,
-                     (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, x);
+                     (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
+                     P.psqt_part, x);
   return hipGetLastError();
 }
 
@@ -448,7 +468,7 @@ hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(plan_scatter_kernel, dim3((n + kScatterPositions - 1) / kScatterPositions), dim3(256), 0, stream,
-                     pos, n, net.psqt_w, P.ctr, P.items, P.flist, P.perm, bucket, psqt);
+                     pos, n, P.ctr, P.items, P.flist, P.perm, bucket, psqt);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint32_t mu = sliced_max_units(n);
 #define CALL(H) ft_slices_t<H>(P, net, x, mu, stream)

@@ -32,9 +32,11 @@ hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* o
                             uint32_t* err, hipStream_t stream);
 
 // Layer stacks: 16 positions per wave, int8 MFMA for fc_0 and fc_1.  Row i of
-// x / bucket is written to positional[perm ? perm[i] : i].
+// x / bucket is written to positional[perm ? perm[i] : i]; when psqt_part is
+// given, psqt[perm[i]] = (psqt_part[2i] - psqt_part[2i+1]) / 2 as well.
 hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net,
-                        int32_t* positional, const uint32_t* perm, hipStream_t stream);
+                        int32_t* positional, const uint32_t* perm, const int32_t* psqt_part, int32_t* psqt,
+                        hipStream_t stream);
 
 // LDS-stationary feature transformer (ft_sliced.hip).
 constexpr uint32_t kUnitItems = 4096;  // perspective-items per (king block) work unit
@@ -45,6 +47,7 @@ struct SlicedPlan {
   uint32_t* items;   // [2 * chunk] item records
   uint16_t* flist;   // [2 * chunk][32] feature rows relative to the king block
   uint32_t* perm;    // [chunk] bucket-sorted slot -> position index
+  int32_t* psqt_part;// [chunk][2] per-slot PSQT sums of the stm / nstm perspective
 };
 size_t sliced_tiles_bytes(uint32_t hd);
 size_t sliced_ctr_words();

@@ -334,7 +334,9 @@ struct StackRegs {
 template <int HD>
 __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ bucket,
                                                     uint32_t n, NetPtrs net, int32_t* __restrict__ positional,
-                                                    const uint32_t* __restrict__ perm) {
+                                                    const uint32_t* __restrict__ perm,
+                                                    const int32_t* __restrict__ psqt_part,
+                                                    int32_t* __restrict__ psqt) {
   constexpr int KS = HD / 64;
   __shared__ __attribute__((aligned(16))) uint8_t x1s[4][16][64];
   __shared__ int32_t fwds[4][16];
@@ -355,6 +357,11 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
     const bool row_ok = prow < n;
     const int bk = row_ok ? bucket[prow] : 0xFF;
     if (row_ok && bk == 0xFF && g == 0) positional[perm ? perm[prow] : prow] = 0;  // invalid position
+    if (psqt_part && row_ok && g == 1) {
+      // upstream transform(): (psqtAcc[stm][b] - psqtAcc[~stm][b]) / 2, int32 wrap then C division
+      const int v = bk == 0xFF ? 0 : (int)((uint32_t)psqt_part[2 * prow] - (uint32_t)psqt_part[2 * prow + 1]) / 2;
+      psqt[perm[prow]] = v;
+    }
     uint32_t bmask = 0;
 #pragma unroll
     for (int b = 0; b < kStacks; ++b)
@@ -458,12 +465,13 @@ hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t n
 
 template <int HD>
 hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net, int32_t* positional,
-                          const uint32_t* perm, hipStream_t stream) {
+                          const uint32_t* perm, const int32_t* psqt_part, int32_t* psqt, hipStream_t stream) {
   const uint32_t tiles = (n + 15) / 16;
   uint32_t blocks = (tiles + 3) / 4;
   if (blocks > 512) blocks = 512;  // persistent: 2 waves per SIMD resident, contiguous tile ranges
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional, perm);
+  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional, perm,
+                     psqt_part, psqt);
   return hipGetLastError();
 }
 
@@ -499,8 +507,9 @@ hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* o
 }
 
 hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net,
-                        int32_t* positional, const uint32_t* perm, hipStream_t stream) {
-#define CALL(H) launch_stack_t<H>(x, bucket, n, net, positional, perm, stream)
+                        int32_t* positional, const uint32_t* perm, const int32_t* psqt_part, int32_t* psqt,
+                        hipStream_t stream) {
+#define CALL(H) launch_stack_t<H>(x, bucket, n, net, positional, perm, psqt_part, psqt, stream)
   FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
 }
