@@ -192,6 +192,39 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
   }
 }
 
+// Writes item `it`'s 32 feature-list entries (rows relative to its king block,
+// padded with the zero row).  ft_slices pairs items 2k and 2k+1 of a pass on
+// one ds_read_b128 lane group; a 128-B tile row r lies in bank half r & 1, so
+// even-position items list their even rows first and odd-position items their
+// odd rows first: the pair then mostly reads opposite bank halves.  A row's
+// parity is (square ^ mirror) & 1 (orient() flips files when the king is on
+// files a-d), and the sum is order-independent.
+__device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ksq, uint32_t it,
+                                           const uint32_t* __restrict__ ctr, uint16_t* __restrict__ flist) {
+  const int kbc = king_block(persp, ksq);
+  const uint32_t pp = (it - ctr[kOff + kbc * 33]) & 1;
+  const uint32_t mirror = (ksq & 7) < 4 ? 1u : 0u;
+  constexpr uint64_t kEvenFiles = 0x5555555555555555ull;
+  uint64_t first = b.occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
+  uint64_t second = b.occ & ~first;
+  uint32_t E[16];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t a = kNoRow;
+    if (first | second) {
+      uint64_t& m = first ? first : second;
+      const int sq = __builtin_ctzll(m);
+      m &= m - 1;
+      a = (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
+    }
+    if (k & 1) E[k >> 1] |= a << 16;
+    else E[k >> 1] = a;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(flist + (size_t)it * 32);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dst[k] = make_uint4(E[4 * k], E[4 * k + 1], E[4 * k + 2], E[4 * k + 3]);
+}
+
 // Item record: (n << 24) | (slot << 1) | half, half 0 = side-to-move half of x.
 // One lane per position; the workgroup's 256 positions get local ranks from
 // LDS atomics, then reserve one range per bin with a single global atomic.
@@ -234,35 +267,8 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
   }
   const int bucket = (b.cnt - 1) >> 2;
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
-  const int kbw = king_block(0, b.wk), kbb = king_block(1, b.bk);
-  uint32_t ew[16], eb[16];
-  uint64_t m = b.occ;
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    uint32_t a = kNoRow, c = kNoRow;
-    if (m) {
-      const int sq = __builtin_ctzll(m);
-      m &= m - 1;
-      const int pc = nibble_at(b.w, sq);
-      const int fw = make_index(0, sq, pc, b.wk), fb = make_index(1, sq, pc, b.bk);
-      a = (uint32_t)(fw - kRowsPerBlock * kbw);
-      c = (uint32_t)(fb - kRowsPerBlock * kbb);
-    }
-    if (k & 1) {
-      ew[k >> 1] |= a << 16;
-      eb[k >> 1] |= c << 16;
-    } else {
-      ew[k >> 1] = a;
-      eb[k >> 1] = c;
-    }
-  }
-  uint4* fw4 = reinterpret_cast<uint4*>(flist + (size_t)iw * 32);
-  uint4* fb4 = reinterpret_cast<uint4*>(flist + (size_t)ib * 32);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    fw4[k] = make_uint4(ew[4 * k], ew[4 * k + 1], ew[4 * k + 2], ew[4 * k + 3]);
-    fb4[k] = make_uint4(eb[4 * k], eb[4 * k + 1], eb[4 * k + 2], eb[4 * k + 3]);
-  }
+  write_rows(b, 0, b.wk, iw, ctr, flist);
+  write_rows(b, 1, b.bk, ib, ctr, flist);
   items[iw] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;
@@ -326,6 +332,48 @@ __device__ __forceinline__ void load_pass(const uint32_t* __restrict__ items, co
   }
 }
 
+// Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
+// 16-byte chunk q of the row).
+template <int G>
+__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], const uint4* img, int q, uint4 (&v)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const uint32_t word = e[2 * G + (t >> 1)];
+    const uint32_t r = min((t & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
+    v[t] = img[r * 8 + q];
+  }
+}
+
+__device__ __forceinline__ void accum_rows(const uint4 (&v)[4], u16x4& lo, u16x4& hi) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    lo += __builtin_bit_cast(u16x4, make_uint2(v[t].x, v[t].y));
+    hi += __builtin_bit_cast(u16x4, make_uint2(v[t].z, v[t].w));
+  }
+}
+
+// NG groups of 4 rows, three groups in flight, no branches: the LDS queue
+// stays fed and hipcc can count lgkmcnt instead of draining it.
+template <int NG, int G = 0>
+__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const uint4* img, int q, uint4 (&v)[3][4],
+                                          u16x4& lo, u16x4& hi) {
+  if constexpr (G < NG) {
+    accum_rows(v[G % 3], lo, hi);
+    if constexpr (G + 3 < NG) issue_rows<G + 3>(e, img, q, v[G % 3]);
+    rows_step<NG, G + 1>(e, img, q, v, lo, hi);
+  }
+}
+
+template <int NG>
+__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const uint4* img, int q, u16x4& lo,
+                                               u16x4& hi) {
+  uint4 v[3][4];
+  issue_rows<0>(e, img, q, v[0]);
+  if constexpr (NG > 1) issue_rows<1>(e, img, q, v[1]);
+  if constexpr (NG > 2) issue_rows<2>(e, img, q, v[2]);
+  rows_step<NG>(e, img, q, v, lo, hi);
+}
+
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; the next
 // pass's records and feature lists are prefetched into registers while the
 // current pass reads the LDS tile.  Items of a unit are sorted by piece count,
@@ -342,7 +390,6 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          int32_t* __restrict__ psqt_part,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
-  constexpr int kRowsPerGroup = 8;
   constexpr int kLastItemLane = 48;
   __shared__ uint4 img[kTileRows * 8];
   __shared__ int32_t ptile[kTileRows * kPsqtBuckets];  // slice 0 only: PSQT rows of the king block
@@ -374,22 +421,16 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
     uint32_t nrec, ne[16];
     load_pass(items, flist, min(base + 16 * 8 + it_in_wave, u.z - 1), nrec, ne);
     u16x4 lo = b_lo, hi = b_hi;
-#pragma unroll
-    for (int g = 0; g < 32 / kRowsPerGroup; ++g) {
-      if (kRowsPerGroup * g < maxn) {
-        uint4 v[kRowsPerGroup];
-#pragma unroll
-        for (int t = 0; t < kRowsPerGroup; ++t) {
-          const uint32_t word = e[(kRowsPerGroup * g + t) >> 1];
-          const uint32_t r = min((t & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
-          v[t] = img[r * 8 + q];
-        }
-#pragma unroll
-        for (int t = 0; t < kRowsPerGroup; ++t) {
-          lo += __builtin_bit_cast(u16x4, make_uint2(v[t].x, v[t].y));
-          hi += __builtin_bit_cast(u16x4, make_uint2(v[t].z, v[t].w));
-        }
-      }
+    switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
+      case 1: rows_pipelined<1>(e, img, q, lo, hi); break;
+      case 2: rows_pipelined<2>(e, img, q, lo, hi); break;
+      case 3: rows_pipelined<3>(e, img, q, lo, hi); break;
+      case 4: rows_pipelined<4>(e, img, q, lo, hi); break;
+      case 5: rows_pipelined<5>(e, img, q, lo, hi); break;
+      case 6: rows_pipelined<6>(e, img, q, lo, hi); break;
+      case 7: rows_pipelined<7>(e, img, q, lo, hi); break;
+      case 8: rows_pipelined<8>(e, img, q, lo, hi); break;
+      default: break;
     }
     const bool valid = base + it_in_wave < u.z;
     if (valid) {
