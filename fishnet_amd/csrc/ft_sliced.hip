@@ -35,7 +35,10 @@ namespace {
 
 constexpr int kRowsPerBlock = 704;            // PS_NB: rows per king block
 constexpr int kTileRows = kRowsPerBlock + 1;  // + one zero row
-constexpr int kNoRow = kRowsPerBlock;         // padding entry -> zero row
+constexpr int kNoRow = kRowsPerBlock;         // the zero row
+// Feature-list entries are 2*row (u16): ft_slices turns an entry into the LDS
+// byte address 128*row + 16*q with one v_mad_u32_u16 (entry * 64 + base).
+constexpr uint32_t kNoEntry = 2 * kNoRow;
 constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
 constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
 constexpr int kBins = kItemBins + kPosBins;
@@ -210,12 +213,12 @@ __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ks
   uint32_t E[16];
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    uint32_t a = kNoRow;
+    uint32_t a = kNoEntry;
     if (first | second) {
       uint64_t& m = first ? first : second;
       const int sq = __builtin_ctzll(m);
       m &= m - 1;
-      a = (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
+      a = 2u * (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
     }
     if (k & 1) E[k >> 1] |= a << 16;
     else E[k >> 1] = a;
@@ -334,44 +337,95 @@ __device__ __forceinline__ void load_pass(const uint32_t* __restrict__ items, co
 
 // Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
 // 16-byte chunk q of the row).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+
+// LDS byte address of the 16-byte chunk of the row named by the low / high
+// u16 entry of `word` (entry = 2*row): entry * 64 + base, base = img + 16*q.
+__device__ __forceinline__ uint32_t row_addr_lo(uint32_t word, uint32_t base) {
+  uint32_t a;
+  asm("v_mad_u32_u16 %0, %1, 64, %2" : "=v"(a) : "v"(word), "v"(base));
+  return a;
+}
+__device__ __forceinline__ uint32_t row_addr_hi(uint32_t word, uint32_t base) {
+  uint32_t a;
+  asm("v_mad_u32_u16 %0, %1, 64, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(word), "v"(base));
+  return a;
+}
+
 template <int G>
-__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], const uint4* img, int q, uint4 (&v)[4]) {
+__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], uint32_t base, u32x4 (&v)[4]) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const uint32_t word = e[2 * G + (t >> 1)];
-    const uint32_t r = min((t & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
-    v[t] = img[r * 8 + q];
+    const uint32_t a = (t & 1) ? row_addr_hi(word, base) : row_addr_lo(word, base);
+    v[t] = *(const lds_u32x4*)(uintptr_t)a;
   }
 }
 
-__device__ __forceinline__ void accum_rows(const uint4 (&v)[4], u16x4& lo, u16x4& hi) {
+__device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4& hi) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    lo += __builtin_bit_cast(u16x4, make_uint2(v[t].x, v[t].y));
-    hi += __builtin_bit_cast(u16x4, make_uint2(v[t].z, v[t].w));
+    lo += __builtin_bit_cast(u16x4, v[t].xy);
+    hi += __builtin_bit_cast(u16x4, v[t].zw);
   }
 }
 
 // NG groups of 4 rows, three groups in flight, no branches: the LDS queue
 // stays fed and hipcc can count lgkmcnt instead of draining it.
 template <int NG, int G = 0>
-__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const uint4* img, int q, uint4 (&v)[3][4],
-                                          u16x4& lo, u16x4& hi) {
+__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], uint32_t base, u32x4 (&v)[3][4], u16x4& lo,
+                                          u16x4& hi) {
   if constexpr (G < NG) {
     accum_rows(v[G % 3], lo, hi);
-    if constexpr (G + 3 < NG) issue_rows<G + 3>(e, img, q, v[G % 3]);
-    rows_step<NG, G + 1>(e, img, q, v, lo, hi);
+    if constexpr (G + 3 < NG) issue_rows<G + 3>(e, base, v[G % 3]);
+    rows_step<NG, G + 1>(e, base, v, lo, hi);
   }
 }
 
 template <int NG>
-__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const uint4* img, int q, u16x4& lo,
-                                               u16x4& hi) {
-  uint4 v[3][4];
-  issue_rows<0>(e, img, q, v[0]);
-  if constexpr (NG > 1) issue_rows<1>(e, img, q, v[1]);
-  if constexpr (NG > 2) issue_rows<2>(e, img, q, v[2]);
-  rows_step<NG>(e, img, q, v, lo, hi);
+__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], uint32_t base, u16x4& lo, u16x4& hi) {
+  u32x4 v[3][4];
+  issue_rows<0>(e, base, v[0]);
+  if constexpr (NG > 1) issue_rows<1>(e, base, v[1]);
+  if constexpr (NG > 2) issue_rows<2>(e, base, v[2]);
+  rows_step<NG>(e, base, v, lo, hi);
+}
+
+// Accumulates one pass (8 items) over the LDS tile: bias + rows, transform,
+// store; in slice 0 also the PSQT part.  maxn = the pass's longest list.
+template <int HD>
+__device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec, int maxn, bool valid, int s, int q,
+                                           uint32_t base, u16x4 b_lo, u16x4 b_hi, const int32_t* ptile,
+                                           int32_t* __restrict__ psqt_part, uint8_t* __restrict__ x) {
+  u16x4 lo = b_lo, hi = b_hi;
+  switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
+    case 1: rows_pipelined<1>(e, base, lo, hi); break;
+    case 2: rows_pipelined<2>(e, base, lo, hi); break;
+    case 3: rows_pipelined<3>(e, base, lo, hi); break;
+    case 4: rows_pipelined<4>(e, base, lo, hi); break;
+    case 5: rows_pipelined<5>(e, base, lo, hi); break;
+    case 6: rows_pipelined<6>(e, base, lo, hi); break;
+    case 7: rows_pipelined<7>(e, base, lo, hi); break;
+    case 8: rows_pipelined<8>(e, base, lo, hi); break;
+    default: break;
+  }
+  const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
+  if (valid) *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
+  if (s == 0) {
+    // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32 wrap).
+    const int bucket = (max((int)(rec >> 24), 1) - 1) >> 2;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      if (k < maxn) {
+        const uint32_t word = e[k >> 1];
+        const uint32_t entry = (k & 1) ? (word >> 16) : (word & 0xFFFF);
+        acc += (uint32_t)ptile[entry * (kPsqtBuckets / 2) + bucket];
+      }
+    }
+    if (valid && q == 0) psqt_part[slot * 2 + half] = (int32_t)acc;
+  }
 }
 
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; the next
@@ -412,50 +466,23 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   lane_item(lane, it_in_wave, q);
   const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
   const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+  const uint32_t lbase = (uint32_t)(uintptr_t)((const lds_u32x4*)img) + 16 * q;
+  // Two register sets: pass A computes from (ra, ea) while (rb, eb) are fetched
+  // for pass B, and vice versa (no copies between passes).
   int base = u.y + wv * 8;
-  uint32_t rec, e[16];
-  load_pass(items, flist, min(base + it_in_wave, u.z - 1), rec, e);
+  uint32_t ra, rb, ea[16], eb[16];
+  load_pass(items, flist, min(base + it_in_wave, u.z - 1), ra, ea);
   __syncthreads();
-  int maxn = (int)(__builtin_amdgcn_readlane(rec, kLastItemLane) >> 24);
-  for (; base < u.z; base += 16 * 8) {
-    uint32_t nrec, ne[16];
-    load_pass(items, flist, min(base + 16 * 8 + it_in_wave, u.z - 1), nrec, ne);
-    u16x4 lo = b_lo, hi = b_hi;
-    switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
-      case 1: rows_pipelined<1>(e, img, q, lo, hi); break;
-      case 2: rows_pipelined<2>(e, img, q, lo, hi); break;
-      case 3: rows_pipelined<3>(e, img, q, lo, hi); break;
-      case 4: rows_pipelined<4>(e, img, q, lo, hi); break;
-      case 5: rows_pipelined<5>(e, img, q, lo, hi); break;
-      case 6: rows_pipelined<6>(e, img, q, lo, hi); break;
-      case 7: rows_pipelined<7>(e, img, q, lo, hi); break;
-      case 8: rows_pipelined<8>(e, img, q, lo, hi); break;
-      default: break;
-    }
-    const bool valid = base + it_in_wave < u.z;
-    if (valid) {
-      const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
-      *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
-    }
-    if (s == 0) {
-      // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32 wrap).
-      const int ni = (int)(rec >> 24);
-      const int bucket = (max(ni, 1) - 1) >> 2;
-      uint32_t acc = 0;
-#pragma unroll
-      for (int k = 0; k < 32; ++k) {
-        if (k < maxn) {
-          const uint32_t word = e[k >> 1];
-          const uint32_t r = min((k & 1) ? (word >> 16) : (word & 0xFFFF), (uint32_t)kNoRow);
-          acc += (uint32_t)ptile[r * kPsqtBuckets + bucket];
-        }
-      }
-      if (valid && q == 0) psqt_part[((rec >> 1) & 0x7FFFFF) * 2 + (rec & 1)] = (int32_t)acc;
-    }
-    rec = nrec;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) e[k] = ne[k];
-    maxn = (int)(__builtin_amdgcn_readlane(rec, kLastItemLane) >> 24);
+  while (base < u.z) {
+    load_pass(items, flist, min(base + 128 + it_in_wave, u.z - 1), rb, eb);
+    slice_pass<HD>(ea, ra, (int)(__builtin_amdgcn_readlane(ra, kLastItemLane) >> 24), base + it_in_wave < u.z, s, q,
+                   lbase, b_lo, b_hi, ptile, psqt_part, x);
+    base += 128;
+    if (base >= u.z) break;
+    load_pass(items, flist, min(base + 128 + it_in_wave, u.z - 1), ra, ea);
+    slice_pass<HD>(eb, rb, (int)(__builtin_amdgcn_readlane(rb, kLastItemLane) >> 24), base + it_in_wave < u.z, s, q,
+                   lbase, b_lo, b_hi, ptile, psqt_part, x);
+    base += 128;
   }
 }
 

@@ -8,9 +8,11 @@ TAG=${1:-rXX}; shift || true
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+[ -n "${SKIP_TRACE:-}" ] || timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
   python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > "$OUT/trace.log" 2>&1
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"; do
+PMCS=${PMCS:-"FETCH_SIZE|WRITE_SIZE|TCC_HIT_sum TCC_MISS_sum|SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"}
+IFS='|' read -ra SETS <<< "$PMCS"
+for pmc in "${SETS[@]}"; do
   name=$(echo "$pmc" | tr ' ' '_')
   timeout -k 10 300 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc_$name" -o run -- \
     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$OUT/pmc_$name.log" 2>&1
