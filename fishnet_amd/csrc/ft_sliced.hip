@@ -36,9 +36,16 @@ namespace {
 constexpr int kRowsPerBlock = 704;            // PS_NB: rows per king block
 constexpr int kTileRows = kRowsPerBlock + 1;  // + one zero row
 constexpr int kNoRow = kRowsPerBlock;         // the zero row
-// Feature-list entries are 2*row (u16): ft_slices turns an entry into the LDS
-// byte address 128*row + 16*q with one v_mad_u32_u16 (entry * 64 + base).
-constexpr uint32_t kNoEntry = 2 * kNoRow;
+// Tile layout, in HBM and in LDS: 8 planes q (16-byte column chunks), each
+// 705 rows x 16 B padded to kPlaneBytes = 11296 = 32 (mod 256).  Chunk q of row
+// r then sits in banks 8q + 4r + [0,4) (mod 64): one row's 8 chunks are
+// conflict-free and rows of opposite parity use complementary banks.
+constexpr int kPlaneBytes = 11296;
+constexpr int kPlaneU4 = kPlaneBytes / 16;    // 706
+constexpr int kTileU4 = 8 * kPlaneU4;         // 5648 x 16 B = 90,368 B
+// Feature-list entries are 16*row (u16), the byte offset of the row inside a
+// plane: ft_slices forms the LDS address base_q + entry with one SDWA add.
+constexpr uint32_t kNoEntry = 16 * kNoRow;
 constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
 constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
 constexpr int kBins = kItemBins + kPosBins;
@@ -218,7 +225,7 @@ __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ks
       uint64_t& m = first ? first : second;
       const int sq = __builtin_ctzll(m);
       m &= m - 1;
-      a = 2u * (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
+      a = 16u * (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
     }
     if (k & 1) E[k >> 1] |= a << 16;
     else E[k >> 1] = a;
@@ -281,20 +288,20 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
 // Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
 // x 705 rows x 8 entries per row.  Single source of truth for the allocation
 // (sliced_tiles_bytes) and the relayout kernel's extent.
-__host__ __device__ constexpr size_t tile_uint4_count(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileRows * 8; }
+__host__ __device__ constexpr size_t tile_uint4_count(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileU4; }
 
 // ---------------------------------------------------------------------------
-// Tile image: tile(kb, s)[r][q] (16 B) = {ft_w[kb*704+r][32s+4q .. +3],
-// ft_w[kb*704+r][HD/2+32s+4q .. +3]}, r = 704 is the zero row.
+// Tile image: tile(kb, s)[q][r] (16 B) = {ft_w[kb*704+r][32s+4q .. +3],
+// ft_w[kb*704+r][HD/2+32s+4q .. +3]}; r = 704 is the zero row, r = 705 padding.
 template <int HD>
 __global__ __launch_bounds__(256) void relayout_kernel(const int16_t* __restrict__ ftw, uint4* __restrict__ tiles) {
   constexpr int S = HD / 64;
   constexpr size_t total = tile_uint4_count(HD);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int q = i & 7;
-    const size_t t = i >> 3;
-    const int r = (int)(t % kTileRows);
-    const size_t ks = t / kTileRows;
+    const int r = (int)(i % kPlaneU4);
+    const size_t t = i / kPlaneU4;
+    const int q = (int)(t & 7);
+    const size_t ks = t >> 3;
     const int s = (int)(ks % S), kb = (int)(ks / S);
     uint4 v = make_uint4(0, 0, 0, 0);
     if (r < kRowsPerBlock) {
@@ -338,43 +345,37 @@ __device__ __forceinline__ void load_pass(const uint32_t* __restrict__ items, co
 // Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
 // 16-byte chunk q of the row).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-// LDS byte address of the 16-byte chunk of the row named by the low / high
-// u16 entry of `word` (entry = 2*row): entry * 64 + base, base = img + 16*q.
-__device__ __forceinline__ uint32_t row_addr_lo(uint32_t word, uint32_t base) {
-  uint32_t a;
-  asm("v_mad_u32_u16 %0, %1, 64, %2" : "=v"(a) : "v"(word), "v"(base));
-  return a;
-}
-__device__ __forceinline__ uint32_t row_addr_hi(uint32_t word, uint32_t base) {
-  uint32_t a;
-  asm("v_mad_u32_u16 %0, %1, 64, %2 op_sel:[1,0,0,0]" : "=v"(a) : "v"(word), "v"(base));
-  return a;
+// LDS byte address of this lane's chunk of the row named by the low / high u16
+// entry of `word`: base (= plane q) + entry; hipcc emits one v_add_u32_sdwa.
+__device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word, int t) {
+  const uint32_t entry = (t & 1) ? (word >> 16) : (word & 0xFFFFu);
+  return static_cast<const u32x4*>(__builtin_assume_aligned(base + entry, 16));
 }
 
 template <int G>
-__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], uint32_t base, u32x4 (&v)[4]) {
+__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], const char* base, u32x4 (&v)[4]) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const uint32_t word = e[2 * G + (t >> 1)];
-    const uint32_t a = (t & 1) ? row_addr_hi(word, base) : row_addr_lo(word, base);
-    v[t] = *(const lds_u32x4*)(uintptr_t)a;
-  }
+  for (int t = 0; t < 4; ++t) v[t] = *row_addr(base, e[2 * G + (t >> 1)], t);
 }
 
 __device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4& hi) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    lo += __builtin_bit_cast(u16x4, v[t].xy);
-    hi += __builtin_bit_cast(u16x4, v[t].zw);
+    // Swizzles go through named temporaries: __builtin_bit_cast of a swizzle
+    // lvalue (v.zw) reads from the vector's base address in this clang.
+    const u32x2 a = __builtin_shufflevector(v[t], v[t], 0, 1);
+    const u32x2 b = __builtin_shufflevector(v[t], v[t], 2, 3);
+    lo += __builtin_bit_cast(u16x4, a);
+    hi += __builtin_bit_cast(u16x4, b);
   }
 }
 
 // NG groups of 4 rows, three groups in flight, no branches: the LDS queue
 // stays fed and hipcc can count lgkmcnt instead of draining it.
 template <int NG, int G = 0>
-__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], uint32_t base, u32x4 (&v)[3][4], u16x4& lo,
+__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[3][4], u16x4& lo,
                                           u16x4& hi) {
   if constexpr (G < NG) {
     accum_rows(v[G % 3], lo, hi);
@@ -384,7 +385,7 @@ __device__ __forceinline__ void rows_step(const uint32_t (&e)[16], uint32_t base
 }
 
 template <int NG>
-__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], uint32_t base, u16x4& lo, u16x4& hi) {
+__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
   u32x4 v[3][4];
   issue_rows<0>(e, base, v[0]);
   if constexpr (NG > 1) issue_rows<1>(e, base, v[1]);
@@ -396,7 +397,7 @@ __device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], uint32_t
 // store; in slice 0 also the PSQT part.  maxn = the pass's longest list.
 template <int HD>
 __device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec, int maxn, bool valid, int s, int q,
-                                           uint32_t base, u16x4 b_lo, u16x4 b_hi, const int32_t* ptile,
+                                           const char* base, u16x4 b_lo, u16x4 b_hi, const int32_t* ptile,
                                            int32_t* __restrict__ psqt_part, uint8_t* __restrict__ x) {
   u16x4 lo = b_lo, hi = b_hi;
   switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
@@ -421,7 +422,7 @@ __device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec
       if (k < maxn) {
         const uint32_t word = e[k >> 1];
         const uint32_t entry = (k & 1) ? (word >> 16) : (word & 0xFFFF);
-        acc += (uint32_t)ptile[entry * (kPsqtBuckets / 2) + bucket];
+        acc += (uint32_t)ptile[(entry >> 4) * kPsqtBuckets + bucket];
       }
     }
     if (valid && q == 0) psqt_part[slot * 2 + half] = (int32_t)acc;
@@ -445,7 +446,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
   constexpr int kLastItemLane = 48;
-  __shared__ uint4 img[kTileRows * 8];
+  __shared__ uint4 img[kTileU4];
   __shared__ int32_t ptile[kTileRows * kPsqtBuckets];  // slice 0 only: PSQT rows of the king block
   const uint32_t w = blockIdx.x;
   const uint32_t j = w >> 3;
@@ -453,8 +454,8 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   const int s = (int)(j % S);
   if (unit >= ctr[kNUnits]) return;
   const int4 u = units[unit];
-  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileRows * 8;
-  for (int i = threadIdx.x; i < kTileRows * 8; i += 1024) img[i] = src[i];
+  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
+  for (int i = threadIdx.x; i < kTileU4; i += 1024) img[i] = src[i];
   if (s == 0) {
     const int32_t* psrc = psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets;
     for (int i = threadIdx.x; i < kTileRows * kPsqtBuckets; i += 1024)
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   lane_item(lane, it_in_wave, q);
   const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
   const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
-  const uint32_t lbase = (uint32_t)(uintptr_t)((const lds_u32x4*)img) + 16 * q;
+  const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
   // Two register sets: pass A computes from (ra, ea) while (rb, eb) are fetched
   // for pass B, and vice versa (no copies between passes).
   int base = u.y + wv * 8;
