@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfnnue.so")
+LIB_PATH = os.environ.get("FNNUE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfnnue.so")
 
 FNNUE_OK = 0
 ERRORS = {

@@ -368,37 +368,57 @@ __device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4
     const u32x2 a = __builtin_shufflevector(v[t], v[t], 0, 1);
     const u32x2 b = __builtin_shufflevector(v[t], v[t], 2, 3);
     lo += __builtin_bit_cast(u16x4, a);
+#ifndef FT_EXP_LO_ONLY
     hi += __builtin_bit_cast(u16x4, b);
+#endif
   }
 }
 
-// NG groups of 4 rows, three groups in flight, no branches: the LDS queue
+#ifndef FT_DEPTH
+#define FT_DEPTH 3
+#endif
+constexpr int kDepth = FT_DEPTH;  // row groups (of 4) in flight per wave
+
+// NG groups of 4 rows, kDepth groups in flight, no branches: the LDS queue
 // stays fed and hipcc can count lgkmcnt instead of draining it.
 template <int NG, int G = 0>
-__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[3][4], u16x4& lo,
-                                          u16x4& hi) {
+__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kDepth][4],
+                                          u16x4& lo, u16x4& hi) {
   if constexpr (G < NG) {
-    accum_rows(v[G % 3], lo, hi);
-    if constexpr (G + 3 < NG) issue_rows<G + 3>(e, base, v[G % 3]);
+    accum_rows(v[G % kDepth], lo, hi);
+    if constexpr (G + kDepth < NG) issue_rows<G + kDepth>(e, base, v[G % kDepth]);
     rows_step<NG, G + 1>(e, base, v, lo, hi);
+  }
+}
+
+template <int NG, int G = 0>
+__device__ __forceinline__ void rows_issue_head(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kDepth][4]) {
+  if constexpr (G < NG && G < kDepth) {
+    issue_rows<G>(e, base, v[G]);
+    rows_issue_head<NG, G + 1>(e, base, v);
   }
 }
 
 template <int NG>
 __device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
-  u32x4 v[3][4];
-  issue_rows<0>(e, base, v[0]);
-  if constexpr (NG > 1) issue_rows<1>(e, base, v[1]);
-  if constexpr (NG > 2) issue_rows<2>(e, base, v[2]);
+#ifndef FT_EXP_NO_ROWS
+  u32x4 v[kDepth][4];
+  rows_issue_head<NG>(e, base, v);
   rows_step<NG>(e, base, v, lo, hi);
+#endif
 }
 
 // Accumulates one pass (8 items) over the LDS tile: bias + rows, transform,
 // store; in slice 0 also the PSQT part.  maxn = the pass's longest list.
+// Both stores are unconditional: a lane past the end of the unit holds the
+// clamped last item and rewrites its identical values, and slices != 0 store
+// their (unused) PSQT word to `trash`.  A store skipped on some path would make
+// hipcc's vmcnt bookkeeping wait for every store before the next pass's rows.
 template <int HD>
-__device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec, int maxn, bool valid, int s, int q,
+__device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec, int maxn, int s, int q,
                                            const char* base, u16x4 b_lo, u16x4 b_hi, const int32_t* ptile,
-                                           int32_t* __restrict__ psqt_part, uint8_t* __restrict__ x) {
+                                           int32_t* __restrict__ psqt_part, int32_t* __restrict__ trash,
+                                           uint8_t* __restrict__ x) {
   u16x4 lo = b_lo, hi = b_hi;
   switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
     case 1: rows_pipelined<1>(e, base, lo, hi); break;
@@ -412,11 +432,11 @@ __device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec
     default: break;
   }
   const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
-  if (valid) *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
+  *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
+  uint32_t acc = 0;
   if (s == 0) {
     // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32 wrap).
     const int bucket = (max((int)(rec >> 24), 1) - 1) >> 2;
-    uint32_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
       if (k < maxn) {
@@ -425,8 +445,8 @@ __device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec
         acc += (uint32_t)ptile[(entry >> 4) * kPsqtBuckets + bucket];
       }
     }
-    if (valid && q == 0) psqt_part[slot * 2 + half] = (int32_t)acc;
   }
+  *(s == 0 ? psqt_part + slot * 2 + half : trash + (threadIdx.x & 63)) = (int32_t)acc;
 }
 
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; the next
@@ -443,6 +463,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          const uint16_t* __restrict__ flist,
                                                          const int32_t* __restrict__ psqw,
                                                          int32_t* __restrict__ psqt_part,
+                                                         int32_t* __restrict__ trash,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
   constexpr int kLastItemLane = 48;
@@ -454,17 +475,25 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   const int s = (int)(j % S);
   if (unit >= ctr[kNUnits]) return;
   const int4 u = units[unit];
-  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
-  for (int i = threadIdx.x; i < kTileU4; i += 1024) img[i] = src[i];
-  if (s == 0) {
-    const int32_t* psrc = psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets;
-    for (int i = threadIdx.x; i < kTileRows * kPsqtBuckets; i += 1024)
-      ptile[i] = i < kRowsPerBlock * kPsqtBuckets ? psrc[i] : 0;
-  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;
   lane_item(lane, it_in_wave, q);
+  // Tile (and PSQT tile) fetch: every load in flight before the first LDS
+  // store, and the first pass's lists behind them, so the fetch costs one
+  // round trip instead of one per 16 KiB.
+  constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
+  constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
+  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
+  uint4 t[kTileLoads];
+#pragma unroll
+  for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
+  uint4 pt[2];
+  const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
+  if (s == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
+  }
   const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
   const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
   const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
@@ -473,16 +502,27 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   int base = u.y + wv * 8;
   uint32_t ra, rb, ea[16], eb[16];
   load_pass(items, flist, min(base + it_in_wave, u.z - 1), ra, ea);
+#pragma unroll
+  for (int k = 0; k < kTileLoads; ++k)
+    if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
+  if (s == 0) {
+    uint4* pdst = reinterpret_cast<uint4*>(ptile);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = (int)threadIdx.x + 1024 * k;
+      if (i < kPtileU4) pdst[i] = i < kPtileRealU4 ? pt[k] : make_uint4(0, 0, 0, 0);
+    }
+  }
   __syncthreads();
   while (base < u.z) {
     load_pass(items, flist, min(base + 128 + it_in_wave, u.z - 1), rb, eb);
-    slice_pass<HD>(ea, ra, (int)(__builtin_amdgcn_readlane(ra, kLastItemLane) >> 24), base + it_in_wave < u.z, s, q,
-                   lbase, b_lo, b_hi, ptile, psqt_part, x);
+    slice_pass<HD>(ea, ra, (int)(__builtin_amdgcn_readlane(ra, kLastItemLane) >> 24), s, q, lbase, b_lo, b_hi,
+                   ptile, psqt_part, trash, x);
     base += 128;
     if (base >= u.z) break;
     load_pass(items, flist, min(base + 128 + it_in_wave, u.z - 1), ra, ea);
-    slice_pass<HD>(eb, rb, (int)(__builtin_amdgcn_readlane(rb, kLastItemLane) >> 24), base + it_in_wave < u.z, s, q,
-                   lbase, b_lo, b_hi, ptile, psqt_part, x);
+    slice_pass<HD>(eb, rb, (int)(__builtin_amdgcn_readlane(rb, kLastItemLane) >> 24), s, q, lbase, b_lo, b_hi,
+                   ptile, psqt_part, trash, x);
     base += 128;
   }
 }
@@ -499,7 +539,7 @@ hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint
   const uint32_t groups = (max_units + 7) / 8;
   hipLaunchKernelGGL((ft_slices_kernel<HD>), dim3(groups * 8 * S), dim3(1024), 0, stream,
                      (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
-                     P.psqt_part, x);
+                     P.psqt_part, P.trash, x);
   return hipGetLastError();
 }
 
