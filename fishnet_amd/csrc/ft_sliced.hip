@@ -325,21 +325,27 @@ __device__ __forceinline__ uint32_t transform4(u16x4 lo, u16x4 hi) {
   return (uint32_t)pr.x | ((uint32_t)pr.y << 8) | ((uint32_t)pr.z << 16) | ((uint32_t)pr.w << 24);
 }
 
-// Loads one pass's item record and its 32 feature rows (16 dwords, two u16
-// each).  The index is clamped into the unit so the loads are unconditional
-// (no exec branch around them: hipcc then counts vmcnt instead of draining it).
-__device__ __forceinline__ void load_pass(const uint32_t* __restrict__ items, const uint16_t* __restrict__ flist,
-                                          int it, uint32_t& rec, uint32_t (&e)[16]) {
-  rec = items[it];
-  const uint4* fl = reinterpret_cast<const uint4*>(flist + (size_t)it * 32);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const uint4 v = fl[k];
-    e[4 * k] = v.x;
-    e[4 * k + 1] = v.y;
-    e[4 * k + 2] = v.z;
-    e[4 * k + 3] = v.w;
-  }
+// One pass's fetch from HBM/L2: this lane's item record, and 8 bytes of the
+// pass's feature lists (lane l: entries 4(l&7) .. +3 of pass item l>>3), so
+// each list byte is fetched once per slice; the lists are then spread to the
+// 8 lanes of each item through a per-wave LDS buffer.  Indices are clamped into
+// the unit so the loads are unconditional (hipcc then counts vmcnt instead of
+// draining it); a clamped lane repeats the unit's last item.
+struct PassFetch {
+  uint32_t rec;
+  uint2 lst;
+};
+__device__ __forceinline__ PassFetch fetch_pass(const uint32_t* __restrict__ items, const uint16_t* __restrict__ flist,
+                                                int pass_base, int last, int lane, int it_in_wave) {
+  PassFetch f;
+  f.rec = items[min(pass_base + it_in_wave, last)];
+  const int li = min(pass_base + (lane >> 3), last);
+#ifdef FT_EXP_NO_LIST
+  f.lst = make_uint2(f.rec & 0x70, f.rec & 0x30);
+#else
+  f.lst = *reinterpret_cast<const uint2*>(flist + (size_t)li * 32 + 4 * (lane & 7));
+#endif
+  return f;
 }
 
 // Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
@@ -408,17 +414,34 @@ __device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const ch
 #endif
 }
 
-// Accumulates one pass (8 items) over the LDS tile: bias + rows, transform,
-// store; in slice 0 also the PSQT part.  maxn = the pass's longest list.
-// Both stores are unconditional: a lane past the end of the unit holds the
-// clamped last item and rewrites its identical values, and slices != 0 store
-// their (unused) PSQT word to `trash`.  A store skipped on some path would make
-// hipcc's vmcnt bookkeeping wait for every store before the next pass's rows.
+// One pass (8 items per wave) over the LDS tile: the lists go to the wave's
+// LDS buffer, bias + rows, transform, store; in slice 0 also the PSQT part.
+// maxn = the pass's longest list.  Both stores are unconditional: a lane past
+// the end of the unit holds the clamped last item and rewrites its identical
+// values, and slices != 0 store their (unused) PSQT word to `trash`.  A store
+// skipped on some path would make hipcc's vmcnt bookkeeping wait for every
+// store before the next pass's rows.
 template <int HD>
-__device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec, int maxn, int s, int q,
-                                           const char* base, u16x4 b_lo, u16x4 b_hi, const int32_t* ptile,
-                                           int32_t* __restrict__ psqt_part, int32_t* __restrict__ trash,
-                                           uint8_t* __restrict__ x) {
+__device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
+                                           int q, const char* base, u16x4 b_lo, u16x4 b_hi,
+                                           const int32_t* ptile, int32_t* __restrict__ psqt_part,
+                                           int32_t* __restrict__ trash, uint8_t* __restrict__ x) {
+  constexpr int kLastItemLane = 48;  // lane_item: lane 48 holds pass item 7, the longest list
+  const uint32_t rec = f.rec;
+  const int maxn = (int)(__builtin_amdgcn_readlane(rec, kLastItemLane) >> 24);
+  // LDS ops of one wave complete in order: this write lands after the previous
+  // pass's reads of lb and before this pass's reads.
+  lb[lane] = f.lst;
+  uint32_t e[16];
+  const uint4* my = reinterpret_cast<const uint4*>(lb) + 4 * it_in_wave;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint4 v = my[m];
+    e[4 * m] = v.x;
+    e[4 * m + 1] = v.y;
+    e[4 * m + 2] = v.z;
+    e[4 * m + 3] = v.w;
+  }
   u16x4 lo = b_lo, hi = b_hi;
   switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
     case 1: rows_pipelined<1>(e, base, lo, hi); break;
@@ -432,28 +455,34 @@ __device__ __forceinline__ void slice_pass(const uint32_t (&e)[16], uint32_t rec
     default: break;
   }
   const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
+#ifdef FT_EXP_NO_STORE
+  if (transform4(lo, hi) == 0x12345678u)
+#endif
   *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
   uint32_t acc = 0;
+#ifdef FT_EXP_NO_PSQT
+  if (false) {
+#else
   if (s == 0) {
-    // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32 wrap).
+#endif
+    // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32
+    // wrap).  The item's 8 lanes take entries q, q+8, q+16, q+24 (padding
+    // entries name the zero row) and reduce over lane masks 1, 2, 12.
     const int bucket = (max((int)(rec >> 24), 1) - 1) >> 2;
+    const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      if (k < maxn) {
-        const uint32_t word = e[k >> 1];
-        const uint32_t entry = (k & 1) ? (word >> 16) : (word & 0xFFFF);
-        acc += (uint32_t)ptile[(entry >> 4) * kPsqtBuckets + bucket];
-      }
-    }
+    for (int j = 0; j < 4; ++j) acc += (uint32_t)ptile[(ent[q + 8 * j] >> 4) * kPsqtBuckets + bucket];
+    acc += (uint32_t)__shfl_xor((int)acc, 1);
+    acc += (uint32_t)__shfl_xor((int)acc, 2);
+    acc += (uint32_t)__shfl_xor((int)acc, 12);
   }
-  *(s == 0 ? psqt_part + slot * 2 + half : trash + (threadIdx.x & 63)) = (int32_t)acc;
+  *(s == 0 ? psqt_part + slot * 2 + half : trash + lane) = (int32_t)acc;
 }
 
-// One workgroup = one (unit, slice).  16 waves x 8 items per pass; the next
-// pass's records and feature lists are prefetched into registers while the
-// current pass reads the LDS tile.  Items of a unit are sorted by piece count,
-// so a pass's longest list is that of its item 7 (clamped into the unit),
-// whose record lane 48 holds (lane_item).
+// One workgroup = one (unit, slice).  16 waves x 8 items per pass; records and
+// lists are fetched two passes ahead while the current pass reads the LDS tile.
+// Items of a unit are sorted by piece count, so a pass's longest list is that
+// of its item 7 (clamped into the unit).
 template <int HD>
 __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict__ tiles,
                                                          const int16_t* __restrict__ ftb,
@@ -466,9 +495,9 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          int32_t* __restrict__ trash,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
-  constexpr int kLastItemLane = 48;
   __shared__ uint4 img[kTileU4];
   __shared__ int32_t ptile[kTileRows * kPsqtBuckets];  // slice 0 only: PSQT rows of the king block
+  __shared__ uint2 lbuf[16][64];                       // per wave: one pass's 8 feature lists
   const uint32_t w = blockIdx.x;
   const uint32_t j = w >> 3;
   const uint32_t unit = (j / S) * 8 + (w & 7);
@@ -480,14 +509,19 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   int it_in_wave, q;
   lane_item(lane, it_in_wave, q);
   // Tile (and PSQT tile) fetch: every load in flight before the first LDS
-  // store, and the first pass's lists behind them, so the fetch costs one
+  // store, and the first passes' lists behind them, so the fetch costs one
   // round trip instead of one per 16 KiB.
   constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
   constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
   const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
   uint4 t[kTileLoads];
 #pragma unroll
-  for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
+  for (int k = 0; k < kTileLoads; ++k)
+#ifdef FT_EXP_NO_TILE
+    t[k] = make_uint4(k, 0, 0, 0);
+#else
+    t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
+#endif
   uint4 pt[2];
   const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
   if (s == 0) {
@@ -497,11 +531,11 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
   const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
   const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
-  // Two register sets: pass A computes from (ra, ea) while (rb, eb) are fetched
-  // for pass B, and vice versa (no copies between passes).
+  uint2* lb = lbuf[wv];
+  const int last = u.z - 1;
   int base = u.y + wv * 8;
-  uint32_t ra, rb, ea[16], eb[16];
-  load_pass(items, flist, min(base + it_in_wave, u.z - 1), ra, ea);
+  PassFetch fa = fetch_pass(items, flist, base, last, lane, it_in_wave);
+  PassFetch fb = fetch_pass(items, flist, base + 128, last, lane, it_in_wave);
 #pragma unroll
   for (int k = 0; k < kTileLoads; ++k)
     if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
@@ -515,14 +549,14 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   }
   __syncthreads();
   while (base < u.z) {
-    load_pass(items, flist, min(base + 128 + it_in_wave, u.z - 1), rb, eb);
-    slice_pass<HD>(ea, ra, (int)(__builtin_amdgcn_readlane(ra, kLastItemLane) >> 24), s, q, lbase, b_lo, b_hi,
-                   ptile, psqt_part, trash, x);
+    const PassFetch cur = fa;
+    fa = fetch_pass(items, flist, base + 256, last, lane, it_in_wave);
+    slice_pass<HD>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, ptile, psqt_part, trash, x);
     base += 128;
     if (base >= u.z) break;
-    load_pass(items, flist, min(base + 128 + it_in_wave, u.z - 1), ra, ea);
-    slice_pass<HD>(eb, rb, (int)(__builtin_amdgcn_readlane(rb, kLastItemLane) >> 24), s, q, lbase, b_lo, b_hi,
-                   ptile, psqt_part, trash, x);
+    const PassFetch cur2 = fb;
+    fb = fetch_pass(items, flist, base + 256, last, lane, it_in_wave);
+    slice_pass<HD>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, ptile, psqt_part, trash, x);
     base += 128;
   }
 }
