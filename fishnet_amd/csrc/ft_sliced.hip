@@ -550,12 +550,16 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   __syncthreads();
   while (base < u.z) {
     const PassFetch cur = fa;
+#ifndef FT_EXP_REUSE_LIST
     fa = fetch_pass(items, flist, base + 256, last, lane, it_in_wave);
+#endif
     slice_pass<HD>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, ptile, psqt_part, trash, x);
     base += 128;
     if (base >= u.z) break;
     const PassFetch cur2 = fb;
+#ifndef FT_EXP_REUSE_LIST
     fb = fetch_pass(items, flist, base + 256, last, lane, it_in_wave);
+#endif
     slice_pass<HD>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, ptile, psqt_part, trash, x);
     base += 128;
   }

@@ -39,7 +39,10 @@ hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, ui
                         hipStream_t stream);
 
 // LDS-stationary feature transformer (ft_sliced.hip).
-constexpr uint32_t kUnitItems = 4096;  // perspective-items per (king block) work unit
+#ifndef FT_UNIT_ITEMS
+#define FT_UNIT_ITEMS 4096
+#endif
+constexpr uint32_t kUnitItems = FT_UNIT_ITEMS;  // perspective-items per (king block) work unit
 constexpr uint32_t kSlicedTrashWords = 64;
 struct SlicedPlan {
   void* tiles;       // [32 king blocks][hd/64 slices][705 rows][8] x 16 B (relayout of ft_w)
