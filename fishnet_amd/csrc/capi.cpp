@@ -144,9 +144,8 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
       hipMalloc(&P.items, (size_t)2 * kChunk * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&P.flist, (size_t)2 * kChunk * 32 * sizeof(uint16_t)) != hipSuccess ||
       hipMalloc(&P.perm, (size_t)kChunk * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&P.psqt_part, ((size_t)2 * kChunk + kSlicedTrashWords) * sizeof(int32_t)) != hipSuccess)
+      hipMalloc(&P.psqt_part, (size_t)2 * kChunk * sizeof(int32_t)) != hipSuccess)
     return fail(FNNUE_E_OOM, "device allocation (sliced plan)");
-  P.trash = P.psqt_part + (size_t)2 * kChunk;
   if (const char* impl = std::getenv("FNNUE_FT_IMPL"))
     c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");

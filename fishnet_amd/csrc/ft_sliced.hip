@@ -46,6 +46,10 @@ constexpr int kTileU4 = 8 * kPlaneU4;         // 5648 x 16 B = 90,368 B
 // Feature-list entries are 16*row (u16), the byte offset of the row inside a
 // plane: ft_slices forms the LDS address base_q + entry with one SDWA add.
 constexpr uint32_t kNoEntry = 16 * kNoRow;
+// Row (within king block kb) of the own-king feature: KingBuckets is a
+// bijection between kb and the oriented king square o on files e-h, and the
+// king plane is 10 (upstream half_ka_v2_hm.h), so every item of kb has it.
+__host__ __device__ constexpr int king_row(int kb) { return 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3)); }
 constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
 constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
 constexpr int kBins = kItemBins + kPosBins;
@@ -203,7 +207,9 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
 }
 
 // Writes item `it`'s 32 feature-list entries (rows relative to its king block,
-// padded with the zero row).  ft_slices pairs items 2k and 2k+1 of a pass on
+// padded with the zero row): every piece except the perspective's own king,
+// whose row is the same for the whole king block (king_row) and is added to
+// the bias once per workgroup instead of once per item.  ft_slices pairs items 2k and 2k+1 of a pass on
 // one ds_read_b128 lane group; a 128-B tile row r lies in bank half r & 1, so
 // even-position items list their even rows first and odd-position items their
 // odd rows first: the pair then mostly reads opposite bank halves.  A row's
@@ -215,8 +221,9 @@ __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ks
   const uint32_t pp = (it - ctr[kOff + kbc * 33]) & 1;
   const uint32_t mirror = (ksq & 7) < 4 ? 1u : 0u;
   constexpr uint64_t kEvenFiles = 0x5555555555555555ull;
-  uint64_t first = b.occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
-  uint64_t second = b.occ & ~first;
+  const uint64_t occ = b.occ & ~(1ull << ksq);  // own king: folded into the bias (king_row)
+  uint64_t first = occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
+  uint64_t second = occ & ~first;
   uint32_t E[16];
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
@@ -314,15 +321,29 @@ __global__ __launch_bounds__(256) void relayout_kernel(const int16_t* __restrict
   }
 }
 
+// Raw buffer resources: num_records = 2^31 - 1 bytes, so any offset >= 2^31
+// fails the bounds check and the store is dropped.  Word 3 = the gfx9-family
+// raw-buffer format (32-bit data format, no swizzle).
+constexpr int kBufferRange = 0x7FFFFFFF;
+constexpr int kBufferFlags = 0x00020000;
+constexpr int kBufferAll = -1;  // num_records = 2^32 - 1: no bounds check in practice
+constexpr uint32_t kDroppedOffset = 0x80000000u;
+
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
+// out byte k = (clamp(lo_k, 0, 127) * clamp(hi_k, 0, 127)) >> 7 (upstream
+// transform).  The doubled product (< 2^15) holds that value in its high byte,
+// so one v_perm_b32 packs the four bytes.
 __device__ __forceinline__ uint32_t transform4(u16x4 lo, u16x4 hi) {
   const s16x4 zero = (s16x4)0, top = (s16x4)127;
   const s16x4 a = __builtin_elementwise_min(__builtin_elementwise_max((s16x4)lo, zero), top);
   const s16x4 b = __builtin_elementwise_min(__builtin_elementwise_max((s16x4)hi, zero), top);
-  const u16x4 pr = ((u16x4)a * (u16x4)b) >> (u16x4)7;
-  return (uint32_t)pr.x | ((uint32_t)pr.y << 8) | ((uint32_t)pr.z << 16) | ((uint32_t)pr.w << 24);
+  const u16x4 pr = ((u16x4)a * (u16x4)b) << (u16x4)1;
+  const u32x2 w = __builtin_bit_cast(u32x2, pr);
+  return __builtin_amdgcn_perm(w.y, w.x, 0x07050301u);
 }
 
 // One pass's fetch from HBM/L2: this lane's item record, and 8 bytes of the
@@ -335,23 +356,22 @@ struct PassFetch {
   uint32_t rec;
   uint2 lst;
 };
-__device__ __forceinline__ PassFetch fetch_pass(const uint32_t* __restrict__ items, const uint16_t* __restrict__ flist,
+__device__ __forceinline__ PassFetch fetch_pass(__amdgpu_buffer_rsrc_t items, __amdgpu_buffer_rsrc_t flist,
                                                 int pass_base, int last, int lane, int it_in_wave) {
   PassFetch f;
-  f.rec = items[min(pass_base + it_in_wave, last)];
-  const int li = min(pass_base + (lane >> 3), last);
+  f.rec = __builtin_amdgcn_raw_buffer_load_b32(items, (uint32_t)min(pass_base + it_in_wave, last) * 4u, 0, 0);
+  const uint32_t li = (uint32_t)min(pass_base + (lane >> 3), last);
 #ifdef FT_EXP_NO_LIST
   f.lst = make_uint2(f.rec & 0x70, f.rec & 0x30);
 #else
-  f.lst = *reinterpret_cast<const uint2*>(flist + (size_t)li * 32 + 4 * (lane & 7));
+  const u32x2 l = __builtin_amdgcn_raw_buffer_load_b64(flist, li * 64u + 8u * (uint32_t)(lane & 7), 0, 0);
+  f.lst = make_uint2(l.x, l.y);
 #endif
   return f;
 }
 
 // Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
 // 16-byte chunk q of the row).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // LDS byte address of this lane's chunk of the row named by the low / high u16
 // entry of `word`: base (= plane q) + entry; hipcc emits one v_add_u32_sdwa.
@@ -363,7 +383,14 @@ __device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word
 template <int G>
 __device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], const char* base, u32x4 (&v)[4]) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) v[t] = *row_addr(base, e[2 * G + (t >> 1)], t);
+  for (int t = 0; t < 4; ++t) {
+    v[t] = *row_addr(base, e[2 * G + (t >> 1)], t);
+#ifdef FT_EXP_DUPREAD
+    const u32x4 extra = *(row_addr(base, e[2 * G + (t >> 1)], t) + 1);
+    uint32_t sink;
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(sink) : "v"(extra.x), "v"(extra.y));
+#endif
+  }
 }
 
 __device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4& hi) {
@@ -374,6 +401,21 @@ __device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4
     const u32x2 a = __builtin_shufflevector(v[t], v[t], 0, 1);
     const u32x2 b = __builtin_shufflevector(v[t], v[t], 2, 3);
     lo += __builtin_bit_cast(u16x4, a);
+#ifdef FT_EXP_EXTRAVALU
+    {
+      uint32_t sink;
+      asm volatile("v_xor_b32 %0, %1, %2" : "=v"(sink) : "v"(a.x), "v"(b.y));
+    }
+#endif
+#ifdef FT_EXP_DUPADD
+    {
+      uint32_t s0, s1, s2, s3;
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s0) : "v"(a.x), "v"(a.y));
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s1) : "v"(a.y), "v"(b.x));
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s2) : "v"(b.x), "v"(b.y));
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s3) : "v"(b.y), "v"(a.x));
+    }
+#endif
 #ifndef FT_EXP_LO_ONLY
     hi += __builtin_bit_cast(u16x4, b);
 #endif
@@ -418,14 +460,14 @@ __device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const ch
 // LDS buffer, bias + rows, transform, store; in slice 0 also the PSQT part.
 // maxn = the pass's longest list.  Both stores are unconditional: a lane past
 // the end of the unit holds the clamped last item and rewrites its identical
-// values, and slices != 0 store their (unused) PSQT word to `trash`.  A store
-// skipped on some path would make hipcc's vmcnt bookkeeping wait for every
-// store before the next pass's rows.
+// values, and slices != 0 issue their PSQT store out of the buffer's bounds
+// (dropped by the hardware).  A store skipped on some path would make hipcc's
+// vmcnt bookkeeping wait for every store before the next pass's rows.
 template <int HD>
 __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
-                                           int q, const char* base, u16x4 b_lo, u16x4 b_hi,
-                                           const int32_t* ptile, int32_t* __restrict__ psqt_part,
-                                           int32_t* __restrict__ trash, uint8_t* __restrict__ x) {
+                                           int q, const char* base, u16x4 b_lo, u16x4 b_hi, int krow,
+                                           const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
+                                           __amdgpu_buffer_rsrc_t x_rsrc) {
   constexpr int kLastItemLane = 48;  // lane_item: lane 48 holds pass item 7, the longest list
   const uint32_t rec = f.rec;
   const int maxn = (int)(__builtin_amdgcn_readlane(rec, kLastItemLane) >> 24);
@@ -443,7 +485,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     e[4 * m + 3] = v.w;
   }
   u16x4 lo = b_lo, hi = b_hi;
-  switch ((maxn + 3) >> 2) {  // wave-uniform; each case is straight-line code
+  switch ((maxn + 2) >> 2) {  // maxn - 1 rows (own king in the bias); wave-uniform, straight-line cases
     case 1: rows_pipelined<1>(e, base, lo, hi); break;
     case 2: rows_pipelined<2>(e, base, lo, hi); break;
     case 3: rows_pipelined<3>(e, base, lo, hi); break;
@@ -454,11 +496,13 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     case 8: rows_pipelined<8>(e, base, lo, hi); break;
     default: break;
   }
-  const uint32_t slot = (rec >> 1) & 0x7FFFFF, half = rec & 1;
+  // (rec & 0xFFFFFF) = 2 * slot + half: times HD/2 it is the offset of the
+  // item's half of row `slot` of x.
+  const uint32_t xoff = (rec & 0xFFFFFFu) * (HD / 2) + 32 * s + 4 * q;
 #ifdef FT_EXP_NO_STORE
   if (transform4(lo, hi) == 0x12345678u)
 #endif
-  *reinterpret_cast<uint32_t*>(x + (size_t)slot * HD + half * (HD / 2) + 32 * s + 4 * q) = transform4(lo, hi);
+  __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xoff, 0, 0);
   uint32_t acc = 0;
 #ifdef FT_EXP_NO_PSQT
   if (false) {
@@ -470,13 +514,18 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     // entries name the zero row) and reduce over lane masks 1, 2, 12.
     const int bucket = (max((int)(rec >> 24), 1) - 1) >> 2;
     const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
+    acc = q == 0 ? (uint32_t)ptile[krow * kPsqtBuckets + bucket] : 0u;  // own king
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc += (uint32_t)ptile[(ent[q + 8 * j] >> 4) * kPsqtBuckets + bucket];
     acc += (uint32_t)__shfl_xor((int)acc, 1);
     acc += (uint32_t)__shfl_xor((int)acc, 2);
     acc += (uint32_t)__shfl_xor((int)acc, 12);
   }
-  *(s == 0 ? psqt_part + slot * 2 + half : trash + lane) = (int32_t)acc;
+  // Slices != 0 address past the buffer's range: the hardware drops the store
+  // (raw buffer bounds check), so every pass issues the same store with no
+  // branch and no memory traffic.
+  const uint32_t poff = s == 0 ? (rec & 0xFFFFFFu) * 4u : kDroppedOffset;
+  __builtin_amdgcn_raw_buffer_store_b32((int32_t)acc, psqt_rsrc, poff, 0, 0);
 }
 
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; records and
@@ -492,7 +541,6 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          const uint16_t* __restrict__ flist,
                                                          const int32_t* __restrict__ psqw,
                                                          int32_t* __restrict__ psqt_part,
-                                                         int32_t* __restrict__ trash,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
   __shared__ uint4 img[kTileU4];
@@ -528,14 +576,21 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
 #pragma unroll
     for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
   }
-  const u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
-  const u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+  u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
+  u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+  const int krow = king_row(u.x);
   const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
   uint2* lb = lbuf[wv];
+  const __amdgpu_buffer_rsrc_t psqt_rsrc = __builtin_amdgcn_make_buffer_rsrc(psqt_part, 0, kBufferRange, kBufferFlags);
+  const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(x, 0, kBufferAll, kBufferFlags);
+  const __amdgpu_buffer_rsrc_t items_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(items), 0, kBufferAll, kBufferFlags);
+  const __amdgpu_buffer_rsrc_t flist_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(flist), 0, kBufferAll, kBufferFlags);
   const int last = u.z - 1;
   int base = u.y + wv * 8;
-  PassFetch fa = fetch_pass(items, flist, base, last, lane, it_in_wave);
-  PassFetch fb = fetch_pass(items, flist, base + 128, last, lane, it_in_wave);
+  PassFetch fa = fetch_pass(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
+  PassFetch fb = fetch_pass(items_rsrc, flist_rsrc, base + 128, last, lane, it_in_wave);
 #pragma unroll
   for (int k = 0; k < kTileLoads; ++k)
     if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
@@ -548,19 +603,25 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
     }
   }
   __syncthreads();
+  {  // the own-king row (every item of the unit has it) joins the bias
+    const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
+    const u32x2 klo = __builtin_shufflevector(kv, kv, 0, 1), khi = __builtin_shufflevector(kv, kv, 2, 3);
+    b_lo += __builtin_bit_cast(u16x4, klo);
+    b_hi += __builtin_bit_cast(u16x4, khi);
+  }
   while (base < u.z) {
     const PassFetch cur = fa;
 #ifndef FT_EXP_REUSE_LIST
-    fa = fetch_pass(items, flist, base + 256, last, lane, it_in_wave);
+    fa = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
 #endif
-    slice_pass<HD>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, ptile, psqt_part, trash, x);
+    slice_pass<HD>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
     base += 128;
     if (base >= u.z) break;
     const PassFetch cur2 = fb;
 #ifndef FT_EXP_REUSE_LIST
-    fb = fetch_pass(items, flist, base + 256, last, lane, it_in_wave);
+    fb = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
 #endif
-    slice_pass<HD>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, ptile, psqt_part, trash, x);
+    slice_pass<HD>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
     base += 128;
   }
 }
@@ -577,7 +638,7 @@ hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint
   const uint32_t groups = (max_units + 7) / 8;
   hipLaunchKernelGGL((ft_slices_kernel<HD>), dim3(groups * 8 * S), dim3(1024), 0, stream,
                      (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
-                     P.psqt_part, P.trash, x);
+                     P.psqt_part, x);
   return hipGetLastError();
 }
 

@@ -43,7 +43,6 @@ hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, ui
 #define FT_UNIT_ITEMS 4096
 #endif
 constexpr uint32_t kUnitItems = FT_UNIT_ITEMS;  // perspective-items per (king block) work unit
-constexpr uint32_t kSlicedTrashWords = 64;
 struct SlicedPlan {
   void* tiles;       // [32 king blocks][hd/64 slices][705 rows][8] x 16 B (relayout of ft_w)
   uint32_t* ctr;     // sliced_ctr_words() counters / offsets
@@ -52,7 +51,6 @@ struct SlicedPlan {
   uint16_t* flist;   // [2 * chunk][32] feature rows relative to the king block
   uint32_t* perm;    // [chunk] bucket-sorted slot -> position index
   int32_t* psqt_part;// [chunk][2] per-slot PSQT sums of the stm / nstm perspective
-  int32_t* trash;    // kSlicedTrashWords words after psqt_part: the PSQT store target of slices != 0
 };
 size_t sliced_tiles_bytes(uint32_t hd);
 size_t sliced_ctr_words();
