@@ -664,8 +664,8 @@ hipError_t launch_relayout_sliced(uint32_t hd, const NetPtrs& net, void* tiles, 
 #undef CALL
 }
 
-hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
-                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+hipError_t launch_sliced_plan(const fnnue_pos* pos, uint32_t n, const SlicedPlan& P, int32_t* psqt, uint8_t* bucket,
+                              uint32_t* err, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
@@ -677,11 +677,22 @@ hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(plan_scatter_kernel, dim3((n + kScatterPositions - 1) / kScatterPositions), dim3(256), 0, stream,
                      pos, n, P.ctr, P.items, P.flist, P.perm, bucket, psqt);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_sliced_ft(uint32_t hd, uint32_t n, const NetPtrs& net, const SlicedPlan& P, uint8_t* x,
+                            hipStream_t stream) {
+  if (n == 0) return hipSuccess;
   const uint32_t mu = sliced_max_units(n);
 #define CALL(H) ft_slices_t<H>(P, net, x, mu, stream)
   FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
+}
+
+hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
+                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+  const hipError_t e = launch_sliced_plan(pos, n, P, psqt, bucket, err, stream);
+  return e != hipSuccess ? e : launch_sliced_ft(hd, n, net, P, x, stream);
 }
 
 }  // namespace fnnue

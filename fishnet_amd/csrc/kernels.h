@@ -56,6 +56,13 @@ size_t sliced_tiles_bytes(uint32_t hd);
 size_t sliced_ctr_words();
 uint32_t sliced_max_units(uint32_t chunk);
 hipError_t launch_relayout_sliced(uint32_t hd, const NetPtrs& net, void* tiles, hipStream_t stream);
+// The two halves of launch_ft_sliced, for pipelining chunks over streams:
+// the plan (psqt[pos] of invalid positions, bucket[slot], P.perm, lists) and
+// the LDS-stationary slices (x[slot], P.psqt_part).
+hipError_t launch_sliced_plan(const fnnue_pos* pos, uint32_t n, const SlicedPlan& P, int32_t* psqt, uint8_t* bucket,
+                              uint32_t* err, hipStream_t stream);
+hipError_t launch_sliced_ft(uint32_t hd, uint32_t n, const NetPtrs& net, const SlicedPlan& P, uint8_t* x,
+                            hipStream_t stream);
 // Writes psqt[pos], x[slot], bucket[slot] and P.perm; then run launch_stack with P.perm.
 hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
                             uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream);

@@ -468,7 +468,10 @@ hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, c
                           const uint32_t* perm, const int32_t* psqt_part, int32_t* psqt, hipStream_t stream) {
   const uint32_t tiles = (n + 15) / 16;
   uint32_t blocks = (tiles + 3) / 4;
-  if (blocks > 512) blocks = 512;  // persistent: 2 waves per SIMD resident, contiguous tile ranges
+#ifndef STACK_BLOCKS
+#define STACK_BLOCKS 512
+#endif
+  if (blocks > STACK_BLOCKS) blocks = STACK_BLOCKS;  // persistent: 2 waves per SIMD resident, contiguous tile ranges
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional, perm,
                      psqt_part, psqt);
