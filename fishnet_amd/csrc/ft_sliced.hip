@@ -53,7 +53,10 @@ __host__ __device__ constexpr int king_row(int kb) { return 640 + 8 * (7 - (kb >
 constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
 constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
 constexpr int kBins = kItemBins + kPosBins;
-constexpr int kScatterPositions = 256;        // positions per plan_scatter workgroup (one per lane)
+#ifndef PLAN_WG
+#define PLAN_WG 1024
+#endif
+constexpr int kScatterPositions = PLAN_WG;    // positions per plan_scatter workgroup (one per lane)
 
 // Counter block layout (uint32 words).
 constexpr int kCnt = 0, kOff = kBins, kCur = 2 * kBins, kNUnits = 3 * kBins;
@@ -245,7 +248,7 @@ __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ks
 // Item record: (n << 24) | (slot << 1) | half, half 0 = side-to-move half of x.
 // One lane per position; the workgroup's 256 positions get local ranks from
 // LDS atomics, then reserve one range per bin with a single global atomic.
-__global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+__global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
                                                            uint32_t* __restrict__ ctr, uint32_t* __restrict__ items,
                                                            uint16_t* __restrict__ flist, uint32_t* __restrict__ perm,
                                                            uint8_t* __restrict__ bucket_out,
@@ -272,7 +275,11 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kBins; i += blockDim.x)
+#ifdef FT_EXP_NO_ATOMIC
+    lbase[i] = lcnt[i] ? ctr[kOff + i] + (blockIdx.x * 7u) % 64u : 0;
+#else
     lbase[i] = lcnt[i] ? atomicAdd(&ctr[kCur + i], lcnt[i]) : 0;
+#endif
   __syncthreads();
   if (!live) return;
   const uint32_t slot = lbase[kp] + rp;
@@ -284,8 +291,10 @@ __global__ __launch_bounds__(256) void plan_scatter_kernel(const fnnue_pos* __re
   }
   const int bucket = (b.cnt - 1) >> 2;
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
+#ifndef FT_EXP_NO_ROWS_WRITE
   write_rows(b, 0, b.wk, iw, ctr, flist);
   write_rows(b, 1, b.bk, ib, ctr, flist);
+#endif
   items[iw] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;
@@ -675,7 +684,7 @@ hipError_t launch_sliced_plan(const fnnue_pos* pos, uint32_t n, const SlicedPlan
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(plan_scatter_kernel, dim3((n + kScatterPositions - 1) / kScatterPositions), dim3(256), 0, stream,
+  hipLaunchKernelGGL(plan_scatter_kernel, dim3((n + kScatterPositions - 1) / kScatterPositions), dim3(kScatterPositions), 0, stream,
                      pos, n, P.ctr, P.items, P.flist, P.perm, bucket, psqt);
   return hipGetLastError();
 }

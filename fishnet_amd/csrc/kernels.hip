@@ -305,17 +305,20 @@ __device__ __forceinline__ int sqr_crelu(int v) {
   return min(127, (int)(((unsigned)(a * a)) >> 19));
 }
 
-// Per-bucket weights as one wave holds them: the whole fc_0 matrix of a layer
-// stack as MFMA B fragments (HD/64 x 16 B per lane), plus fc_1/fc_2 pieces.
-template <int HD>
+// Per-bucket weights as one wave holds them: fc_1/fc_2 pieces and, unless the
+// kernel keeps all fc_0 matrices in LDS (kW0InLds), the fc_0 matrix of the
+// current layer stack as MFMA B fragments (HD/64 x 16 B per lane).
+template <int HD, bool kW0InLds>
 struct StackRegs {
-  v4i w0[HD / 64];
+  v4i w0[kW0InLds ? 1 : HD / 64];
   v4i w1a, w1b;
   int b0, b1a, b1b, w2a, w2b, b2;
   __device__ __forceinline__ void load(const NetPtrs& net, int b, int r16, int g) {
-    const v4i* wr = reinterpret_cast<const v4i*>(net.w0 + ((size_t)b * kL2 + r16) * HD);
+    if constexpr (!kW0InLds) {
+      const v4i* wr = reinterpret_cast<const v4i*>(net.w0 + ((size_t)b * kL2 + r16) * HD);
 #pragma unroll
-    for (int s = 0; s < HD / 64; ++s) w0[s] = wr[4 * s + g];
+      for (int s = 0; s < HD / 64; ++s) w0[s] = wr[4 * s + g];
+    }
     const int8_t* w1 = net.w1 + (size_t)b * kL3 * kFc1In;
     w1a = g < 2 ? *reinterpret_cast<const v4i*>(w1 + r16 * kFc1In + 16 * g) : (v4i)0;
     w1b = g < 2 ? *reinterpret_cast<const v4i*>(w1 + (16 + r16) * kFc1In + 16 * g) : (v4i)0;
@@ -328,28 +331,56 @@ struct StackRegs {
   }
 };
 
+// fc_0 weights of all 8 layer stacks in LDS (HD <= 1024: 128 KiB), one
+// 1024-thread workgroup per CU, so 4 waves per SIMD stream x instead of the 2
+// that fit when every wave holds a 16 KiB fc_0 matrix in VGPRs.  16-B chunk c
+// of row (b, o) lives at chunk c ^ (o & (chunks - 1)): the 16 rows one
+// ds_read_b128 lane group reads at a fixed K offset then cover all 64 banks.
+template <int HD>
+struct W0Lds {
+  static constexpr bool kOn = HD <= 1024;
+  static constexpr int kChunks = HD / 16;
+  static constexpr int kWords = kOn ? kStacks * kL2 * kChunks : 1;
+  // waves per workgroup: the x tile takes HD/16 VGPRs per lane, so HD = 1024
+  // runs 3 waves per SIMD (<= 168 VGPRs) rather than 4 with spills
+  static constexpr int kWaves = !kOn ? 4 : HD <= 512 ? 16 : 12;
+  __device__ static __forceinline__ int slot(int b, int o, int c) {
+    return (b * kL2 + o) * kChunks + (c ^ (o & (kChunks - 1)));
+  }
+};
+
 // Persistent waves; wave w owns a contiguous range of 16-row tiles.  Rows come
 // bucket-sorted from the sliced FT (perm != null), so a wave's weights stay in
-// VGPRs across tiles and are reloaded only when the bucket changes.
+// registers (LDS) across tiles and are reloaded only when the bucket changes.
 template <int HD>
-__global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ x, const uint8_t* __restrict__ bucket,
-                                                    uint32_t n, NetPtrs net, int32_t* __restrict__ positional,
-                                                    const uint32_t* __restrict__ perm,
-                                                    const int32_t* __restrict__ psqt_part,
-                                                    int32_t* __restrict__ psqt) {
+__global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
+    const uint8_t* __restrict__ x, const uint8_t* __restrict__ bucket, uint32_t n, NetPtrs net,
+    int32_t* __restrict__ positional, const uint32_t* __restrict__ perm, const int32_t* __restrict__ psqt_part,
+    int32_t* __restrict__ psqt) {
   constexpr int KS = HD / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t x1s[4][16][64];
-  __shared__ int32_t fwds[4][16];
+  constexpr bool kLds = W0Lds<HD>::kOn;
+  constexpr int kWaves = W0Lds<HD>::kWaves;
+  __shared__ v4i w0s[W0Lds<HD>::kWords];
+  __shared__ __attribute__((aligned(16))) uint8_t x1s[kWaves][16][64];
+  __shared__ int32_t fwds[kWaves][16];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
+  if constexpr (kLds) {
+    const v4i* src = reinterpret_cast<const v4i*>(net.w0);
+    for (int i = threadIdx.x; i < W0Lds<HD>::kWords; i += blockDim.x) {
+      const int c = i % W0Lds<HD>::kChunks, row = i / W0Lds<HD>::kChunks;
+      w0s[W0Lds<HD>::slot(row / kL2, row % kL2, c)] = src[i];
+    }
+  }
   // Zero the fc_1 input tile once (k >= 30 stays zero).
   *reinterpret_cast<v4i*>(&x1s[wv][r16][16 * g]) = (v4i)0;
-  wave_lds_sync();
+  if constexpr (kLds) __syncthreads();
+  else wave_lds_sync();
   const uint32_t ntiles = (n + 15) / 16;
-  const uint32_t nw = gridDim.x * 4, wid = blockIdx.x * 4 + wv;
+  const uint32_t nw = gridDim.x * kWaves, wid = blockIdx.x * kWaves + wv;
   const uint32_t per = (ntiles + nw - 1) / nw;
   const uint32_t t_begin = wid * per, t_end = min(ntiles, t_begin + per);
-  StackRegs<HD> W;
+  StackRegs<HD, kLds> W;
   int cur = -1;
   for (uint32_t tile = t_begin; tile < t_end; ++tile) {
     const uint32_t p0 = tile * 16;
@@ -380,7 +411,12 @@ __global__ __launch_bounds__(256) void stack_kernel(const uint8_t* __restrict__ 
       // fc_0: y[pos][out] = b0 + sum_k x[pos][k] * w0[out][k]
       v4i acc = (v4i)0;
 #pragma unroll
-      for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], W.w0[s], acc, 0, 0, 0);
+      for (int s = 0; s < KS; ++s) {
+        v4i wf;
+        if constexpr (kLds) wf = w0s[W0Lds<HD>::slot(b, r16, 4 * s + g)];
+        else wf = W.w0[s];
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[s], wf, acc, 0, 0, 0);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int y = acc[r] + W.b0;
@@ -466,15 +502,15 @@ hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t n
 template <int HD>
 hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, const NetPtrs& net, int32_t* positional,
                           const uint32_t* perm, const int32_t* psqt_part, int32_t* psqt, hipStream_t stream) {
+  // Persistent, contiguous tile ranges: HD <= 1024 one workgroup per CU (fc_0
+  // in LDS), else two 4-wave workgroups per CU (fc_0 in VGPRs).
+  constexpr uint32_t kWaves = W0Lds<HD>::kWaves, kMaxBlocks = W0Lds<HD>::kOn ? 256 : 512;
   const uint32_t tiles = (n + 15) / 16;
-  uint32_t blocks = (tiles + 3) / 4;
-#ifndef STACK_BLOCKS
-#define STACK_BLOCKS 512
-#endif
-  if (blocks > STACK_BLOCKS) blocks = STACK_BLOCKS;  // persistent: 2 waves per SIMD resident, contiguous tile ranges
+  uint32_t blocks = (tiles + kWaves - 1) / kWaves;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(256), 0, stream, x, bucket, n, net, positional, perm,
-                     psqt_part, psqt);
+  hipLaunchKernelGGL((stack_kernel<HD>), dim3(blocks), dim3(64 * kWaves), 0, stream, x, bucket, n, net, positional,
+                     perm, psqt_part, psqt);
   return hipGetLastError();
 }
 
