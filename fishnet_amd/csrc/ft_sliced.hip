@@ -133,7 +133,7 @@ __device__ __forceinline__ int nibble_at(const uint32_t (&w)[8], int s) {
   return (int)((((i & 4) ? hi : lo) >> (4 * (s & 7))) & 15u);
 }
 
-__global__ __launch_bounds__(256) void plan_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+__global__ __launch_bounds__(1024) void plan_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
                                                          uint32_t* __restrict__ ctr, uint32_t* __restrict__ err) {
   __shared__ uint32_t h[kBins];
   for (int i = threadIdx.x; i < kBins; i += blockDim.x) h[i] = 0;
@@ -197,15 +197,22 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
     ctr[kOff + i] = s[i];
     ctr[kCur + i] = s[i];
   }
-  if (t == 0) {
-    // Unit table: each king block's item range in chunks of <= unit_items.
-    uint32_t nu = 0;
-    for (int kb = 0; kb < 32; ++kb) {
-      const uint32_t b = s[kb * 33];
-      const uint32_t e = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
-      for (uint32_t c = b; c < e; c += unit_items) units[nu++] = make_int4(kb, (int)c, (int)min(e, c + unit_items), 0);
+  if (t < 32) {
+    // Unit table: each king block's item range in chunks of <= unit_items;
+    // lane kb counts its block's units, a wave prefix sum places them.
+    const int kb = t;
+    const uint32_t b = s[kb * 33];
+    const uint32_t e = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
+    const uint32_t mine = (e - b + unit_items - 1) / unit_items;
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 32);
+      if (kb >= o) incl += v;
     }
-    ctr[kNUnits] = nu;
+    uint32_t nu = incl - mine;
+    for (uint32_t c = b; c < e; c += unit_items) units[nu++] = make_int4(kb, (int)c, (int)min(e, c + unit_items), 0);
+    if (kb == 31) ctr[kNUnits] = incl;
   }
 }
 
@@ -678,9 +685,11 @@ hipError_t launch_sliced_plan(const fnnue_pos* pos, uint32_t n, const SlicedPlan
   if (n == 0) return hipSuccess;
   hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
   if (e != hipSuccess) return e;
-  uint32_t blocks = (n + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(plan_count_kernel, dim3(blocks), dim3(256), 0, stream, pos, n, P.ctr, err);
+  // 1024-thread workgroups, at most one per CU: the per-bin global atomics that
+  // merge the LDS histograms scale with the number of workgroups.
+  uint32_t blocks = (n + 1023) / 1024;
+  if (blocks > 256) blocks = 256;
+  hipLaunchKernelGGL(plan_count_kernel, dim3(blocks), dim3(1024), 0, stream, pos, n, P.ctr, err);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
   if ((e = hipGetLastError()) != hipSuccess) return e;
