@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
+VALU_PEAK = 256 * 4 * 2.4e9 / 4  # VOP3-class wave64 instructions/s: 1024 SIMDs, 4 cycles each at 2.4 GHz
 METRIC = "NNUE positions evaluated/sec (1–8 MI355X) + % HBM roofline, bit-exact"
 PSQT_BUCKETS = 8
 
@@ -221,13 +222,22 @@ def main():
 
     # roofline.traffic: PMC-measured bytes per launch of the same workload, from the
     # committed profile (tools/profile.sh + tools/traffic.py -> profiles/traffic.json).
-    traffic, traffic_src = None, None
+    traffic, traffic_src, issue = None, None, None
     tkey = f"{args.workload}:{args.ft_impl if off is None else 'groups'}:hd{args.hd}"
     tpath = os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
         entry = json.load(open(tpath)).get(tkey)
         if entry:
             traffic, traffic_src = entry["bytes_per_launch"], entry["source"]
+            if entry.get("valu_insts_per_launch"):
+                # The sliced FT moves ~2% of its algorithmic bytes through HBM; what bounds
+                # it is vector-instruction issue: SQ_INSTS_VALU per launch
+                # (committed PMC profile) over the live kernel time, against one
+                # 64-bit-encoded (VOP3/VOP3P/SDWA) wave64 VALU instruction per 4 cycles
+                # per SIMD at the 2.4 GHz spec clock (tools/diag/valu_bench.hip).
+                rate = entry["valu_insts_per_launch"] / (ft_avg_ms * 1e-3)
+                issue = {"unit": "VALU instr/s", "achieved": round(rate, -6), "peak": VALU_PEAK,
+                         "frac": round(rate / VALU_PEAK, 4), "source": traffic_src}
 
     if rank == 0:
         out = {
@@ -259,6 +269,7 @@ def main():
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "issue": issue,
                 "kernel": ("ft_slices_kernel + plan_* (LDS-stationary FT)" if off is None and args.ft_impl == "sliced"
                            else "ft_scratch_kernel" if off is None else "ft_groups_kernel"),
                 "kernel_avg_ms": round(ft_avg_ms, 4),
