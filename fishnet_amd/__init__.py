@@ -2,6 +2,6 @@
 analysis path (HIP/CDNA4 kernels behind the C ABI in include/fnnue.h)."""
 from .nnue import (  # noqa: F401
     Evaluator, FnnueError, Net, device_count, game_children, game_positions, perft, pos_from_fen,
-    random_playouts, selftest_mfma, synthesize_net,
+    pack_games, random_game, random_playouts, selftest_mfma, synthesize_net,
 )
 from ._native import GROUP_CHAIN, GROUP_STAR, PLAYOUT_CHILDREN, PLAYOUT_FINAL, PLAYOUT_PLIES  # noqa: F401

@@ -1,0 +1,51 @@
+// builder.h — device-side batch builder (builder.hip): FEN parse, UCI replay
+// and legal children on the GPU.  Same semantics as the host builder
+// (board.h / board.cpp), which the tests hold it to record for record.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/fnnue.h"
+#include "board.h"
+
+namespace fnnue {
+
+__host__ __device__ inline int make_piece_d(int c, int pt) { return (c << 3) | pt; }
+
+// Board state a ply needs for move generation: bitboards, castling rooks
+// ([colour][0 king side, 1 queen side], -1 none), en-passant square.
+struct DBoard {
+  uint64_t bc[2];   // by colour
+  uint64_t bt[7];   // by piece type (1..6), [0] unused
+  int8_t cr[2][2];
+  int8_t ep;
+  uint8_t stm;
+  uint8_t c960;     // castling rights need Chess960 notation (non-standard rook/king files)
+  uint8_t pad[1];
+};
+
+DBoard to_dboard(const Board& b);
+
+constexpr uint32_t kBuildErrFen = 1, kBuildErrMove = 2;
+
+struct BuildResult {
+  hipError_t hip = hipSuccess;
+  bool capacity = false;   // outputs too small: n_out / n_groups say what is needed
+  size_t n_out = 0, n_groups = 0;
+  uint32_t err_code = 0, err_game = 0, err_ply = 0;  // kBuildErr*: first failing game, ply (1-based move)
+};
+
+// text: game g's FEN in [fen_off[g], mv_off[g]), its space-separated UCI moves
+// in [mv_off[g], fen_off[g + 1]).  children = false: every ply of every game,
+// group g = game g; children = true: one group per ply = the ply's position
+// followed by its legal children (Board::legal_moves order).  Synchronises `s`.
+BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                               uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
+                               size_t off_cap, hipStream_t s);
+
+// Leaf count of perft(depth) summed over the frontier boards (1 <= depth <= 3).
+hipError_t perft_device(const std::vector<DBoard>& frontier, int depth, uint64_t* nodes);
+
+}  // namespace fnnue

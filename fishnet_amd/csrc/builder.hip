@@ -1,0 +1,635 @@
+// builder.hip — device-side batch builder: FEN parse, UCI-move replay
+// (standard + Chess960 castling, en passant, promotion) and legal 1-ply
+// children, producing packed fnnue_pos records in HBM.
+//
+// Replaces on the device what board.cpp does on the host, i.e. the role
+// shakmaty 0.23.0 plays in the reference's batch expansion
+// ([ref] src/queue.rs:518-627: VariantPosition::from_setup, Uci::to_move,
+// play_unchecked; wire format src/api.rs:293-309).  Semantics are those of the
+// host builder (board.cpp), which is perft-checked; tests compare the two
+// record for record, and fnnue_perft_device pins the move generator on the
+// published perft counts.
+//
+// Work is one thread per game (FEN parse + replay: each ply depends on the
+// previous) and one thread per ply (children).  Boards are bitboards in
+// registers: no tables, attacks from shifts and ray walks.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "board.h"
+#include "builder.h"
+
+namespace fnnue {
+
+namespace {
+
+constexpr uint64_t kNotA = 0xFEFEFEFEFEFEFEFEull, kNotH = 0x7F7F7F7F7F7F7F7Full;
+constexpr uint64_t kNotAB = 0xFCFCFCFCFCFCFCFCull, kNotGH = 0x3F3F3F3F3F3F3F3Full;
+
+__device__ __forceinline__ int lsb(uint64_t b) { return __builtin_ctzll(b); }
+
+__device__ __forceinline__ uint64_t knight_att(int s) {
+  const uint64_t b = 1ull << s;
+  return ((b << 17) & kNotA) | ((b << 15) & kNotH) | ((b << 10) & kNotAB) | ((b << 6) & kNotGH) |
+         ((b >> 17) & kNotH) | ((b >> 15) & kNotA) | ((b >> 10) & kNotGH) | ((b >> 6) & kNotAB);
+}
+
+__device__ __forceinline__ uint64_t king_att(int s) {
+  const uint64_t b = 1ull << s;
+  return ((b << 1) & kNotA) | ((b >> 1) & kNotH) | (b << 8) | (b >> 8) | ((b << 9) & kNotA) | ((b << 7) & kNotH) |
+         ((b >> 7) & kNotA) | ((b >> 9) & kNotH);
+}
+
+// Squares a pawn of colour c on s attacks.
+__device__ __forceinline__ uint64_t pawn_att(int c, int s) {
+  const uint64_t b = 1ull << s;
+  return c == WHITE ? ((b << 9) & kNotA) | ((b << 7) & kNotH) : ((b >> 7) & kNotA) | ((b >> 9) & kNotH);
+}
+
+__device__ __forceinline__ uint64_t ray(int s, int dr, int df, uint64_t occ) {
+  uint64_t a = 0;
+  int r = (s >> 3) + dr, f = (s & 7) + df;
+  while (r >= 0 && r < 8 && f >= 0 && f < 8) {
+    const int t = r * 8 + f;
+    a |= 1ull << t;
+    if (occ & (1ull << t)) break;
+    r += dr;
+    f += df;
+  }
+  return a;
+}
+
+__device__ __forceinline__ uint64_t bishop_att(int s, uint64_t occ) {
+  return ray(s, 1, 1, occ) | ray(s, 1, -1, occ) | ray(s, -1, 1, occ) | ray(s, -1, -1, occ);
+}
+__device__ __forceinline__ uint64_t rook_att(int s, uint64_t occ) {
+  return ray(s, 1, 0, occ) | ray(s, -1, 0, occ) | ray(s, 0, 1, occ) | ray(s, 0, -1, occ);
+}
+
+struct DMove {
+  int from, to, promo, castle;  // castle: to = rook square (king takes rook)
+};
+
+__device__ __forceinline__ int piece_at(const DBoard& b, int s) {
+  const uint64_t m = 1ull << s;
+  if (!((b.bc[0] | b.bc[1]) & m)) return 0;
+  const int c = (b.bc[1] & m) ? 1 : 0;
+  int t = 1;
+  while (t < KING && !(b.bt[t] & m)) ++t;
+  return make_piece_d(c, t);
+}
+
+__device__ __forceinline__ void put(DBoard& b, int s, int pc) {
+  const uint64_t m = 1ull << s;
+  b.bc[pc >> 3] |= m;
+  b.bt[pc & 7] |= m;
+}
+
+__device__ __forceinline__ void remove_sq(DBoard& b, int s) {
+  const uint64_t m = ~(1ull << s);
+  b.bc[0] &= m;
+  b.bc[1] &= m;
+#pragma unroll
+  for (int t = 1; t < 7; ++t) b.bt[t] &= m;
+}
+
+__device__ __forceinline__ int king_sq(const DBoard& b, int c) {
+  const uint64_t k = b.bt[KING] & b.bc[c];
+  return k ? lsb(k) : -1;
+}
+
+__device__ __noinline__ bool attacked(const DBoard& b, int s, int by, uint64_t occ) {
+  const uint64_t them = b.bc[by];
+  if (pawn_att(by ^ 1, s) & b.bt[PAWN] & them) return true;
+  if (knight_att(s) & b.bt[KNIGHT] & them) return true;
+  if (king_att(s) & b.bt[KING] & them) return true;
+  if (bishop_att(s, occ) & (b.bt[BISHOP] | b.bt[QUEEN]) & them) return true;
+  if (rook_att(s, occ) & (b.bt[ROOK] | b.bt[QUEEN]) & them) return true;
+  return false;
+}
+
+// Board::do_move (board.cpp), on bitboards.
+__device__ __noinline__ void do_move(DBoard& b, const DMove& m) {
+  const int us = b.stm;
+  const int pc = piece_at(b, m.from);
+  const int back = us == WHITE ? 0 : 56;
+  int new_ep = -1;
+  if (m.castle) {
+    const bool king_side = m.to > m.from;
+    const int kto = back + (king_side ? 6 : 2), rto = back + (king_side ? 5 : 3);
+    const int rook = piece_at(b, m.to);
+    remove_sq(b, m.from);
+    remove_sq(b, m.to);
+    put(b, kto, pc);
+    put(b, rto, rook);
+    b.cr[us][0] = b.cr[us][1] = -1;
+  } else {
+    remove_sq(b, m.to);
+    if ((pc & 7) == PAWN) {
+      if (m.to == b.ep && (m.from & 7) != (m.to & 7)) remove_sq(b, m.to + (us == WHITE ? -8 : 8));
+      if ((m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
+    }
+    remove_sq(b, m.from);
+    put(b, m.to, m.promo ? make_piece_d(us, m.promo) : pc);
+    if ((pc & 7) == KING) b.cr[us][0] = b.cr[us][1] = -1;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int side = 0; side < 2; ++side)
+        if (b.cr[c][side] == m.from || b.cr[c][side] == m.to) b.cr[c][side] = -1;
+  }
+  b.ep = (int8_t)new_ep;
+  b.stm = (uint8_t)(us ^ 1);
+}
+
+__device__ __noinline__ bool legal(const DBoard& b, const DMove& m) {
+  DBoard c = b;
+  do_move(c, m);
+  const int k = king_sq(c, b.stm);
+  return k >= 0 && !attacked(c, k, b.stm ^ 1, c.bc[0] | c.bc[1]);
+}
+
+// Legal moves in the order of Board::pseudo_moves + is_legal (board.cpp):
+// own pieces by square; a pawn's push (promotions Q, R, B, N), double push,
+// captures by square, en passant; then castling king side, queen side.
+// f(move) returns false to stop early.
+template <class F>
+__device__ void for_each_legal(const DBoard& b, F&& f) {
+  const int us = b.stm, them = us ^ 1;
+  const uint64_t occ = b.bc[0] | b.bc[1], own = b.bc[us], opp = b.bc[them];
+  const int up = us == WHITE ? 8 : -8;
+  const int rank7 = us == WHITE ? 6 : 1, rank2 = us == WHITE ? 1 : 6;
+  auto emit = [&](int from, int to, int promo, int castle) -> bool {
+    const DMove m{from, to, promo, castle};
+    return !legal(b, m) || f(m);
+  };
+  for (uint64_t pcs = own; pcs; pcs &= pcs - 1) {
+    const int s = lsb(pcs);
+    const uint64_t sm = 1ull << s;
+    if (b.bt[PAWN] & sm) {
+      const bool promo = (s >> 3) == rank7;
+      auto pawn_to = [&](int t) -> bool {
+        if (promo) {
+          for (int p = QUEEN; p >= KNIGHT; --p)
+            if (!emit(s, t, p, 0)) return false;
+          return true;
+        }
+        return emit(s, t, 0, 0);
+      };
+      const int t1 = s + up;
+      if (!(occ & (1ull << t1))) {
+        if (!pawn_to(t1)) return;
+        const int t2 = t1 + up;
+        if ((s >> 3) == rank2 && !(occ & (1ull << t2)) && !emit(s, t2, 0, 0)) return;
+      }
+      for (uint64_t a = pawn_att(us, s) & opp; a; a &= a - 1)
+        if (!pawn_to(lsb(a))) return;
+      if (b.ep >= 0 && (pawn_att(us, s) & (1ull << b.ep)) && !emit(s, b.ep, 0, 0)) return;
+      continue;
+    }
+    uint64_t targets;
+    if (b.bt[KNIGHT] & sm) targets = knight_att(s);
+    else if (b.bt[BISHOP] & sm) targets = bishop_att(s, occ);
+    else if (b.bt[ROOK] & sm) targets = rook_att(s, occ);
+    else if (b.bt[QUEEN] & sm) targets = bishop_att(s, occ) | rook_att(s, occ);
+    else targets = king_att(s);
+    for (uint64_t t = targets & ~own; t; t &= t - 1)
+      if (!emit(s, lsb(t), 0, 0)) return;
+  }
+  const int ksq = king_sq(b, us);
+  const int back = us == WHITE ? 0 : 56;
+  if (ksq < 0 || (ksq & 56) != back) return;
+  for (int side = 0; side < 2; ++side) {
+    const int rsq = b.cr[us][side];
+    if (rsq < 0 || piece_at(b, rsq) != make_piece_d(us, ROOK)) continue;
+    const int kto = back + (side == 0 ? 6 : 2), rto = back + (side == 0 ? 5 : 3);
+    const int lo = min(min(ksq, rsq), min(kto, rto)), hi = max(max(ksq, rsq), max(kto, rto));
+    bool ok = true;
+    for (int t = lo; t <= hi && ok; ++t)
+      if (t != ksq && t != rsq && (occ & (1ull << t))) ok = false;
+    if (!ok || attacked(b, ksq, them, occ)) continue;
+    const int step = kto > ksq ? 1 : -1;
+    for (int t = ksq; t != kto && ok;) {
+      t += step;
+      if (attacked(b, t, them, occ)) ok = false;
+    }
+    if (ok && !emit(ksq, rsq, 0, 1)) return;  // legal() re-checks the king; castling already is
+  }
+}
+
+__device__ __noinline__ fnnue_pos pack(const DBoard& b) {
+  fnnue_pos p;
+  uint32_t w[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) w[i] = 0;
+  for (uint64_t o = b.bc[0] | b.bc[1]; o; o &= o - 1) {
+    const int s = lsb(o);
+    w[s >> 3] |= (uint32_t)piece_at(b, s) << (4 * (s & 7));
+  }
+  w[8] = b.stm;
+  memcpy(&p, w, sizeof(p));
+  return p;
+}
+
+// ---- text ----
+__device__ __forceinline__ bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+// Next whitespace-separated token of [*p, end): returns its length (0 = none).
+__device__ __forceinline__ int next_token(const char* text, uint32_t& p, uint32_t end, uint32_t& start) {
+  while (p < end && is_space(text[p])) ++p;
+  start = p;
+  while (p < end && !is_space(text[p])) ++p;
+  return (int)(p - start);
+}
+
+__device__ __forceinline__ int count_tokens(const char* text, uint32_t p, uint32_t end) {
+  int n = 0;
+  uint32_t st;
+  while (next_token(text, p, end, st) > 0) ++n;
+  return n;
+}
+
+// board_from_fen (board.cpp) on the device.  Returns false on malformed FEN.
+__device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t end, DBoard& b) {
+  for (int i = 0; i < 2; ++i) b.bc[i] = 0;
+  for (int i = 0; i < 7; ++i) b.bt[i] = 0;
+  b.cr[0][0] = b.cr[0][1] = b.cr[1][0] = b.cr[1][1] = -1;
+  b.ep = -1;
+  b.stm = WHITE;
+  b.c960 = 0;
+  uint32_t st;
+  int len = next_token(text, p, end, st);
+  if (len == 0) return false;
+  int r = 7, f = 0;
+  for (uint32_t i = st; i < st + (uint32_t)len; ++i) {
+    const char ch = text[i];
+    if (ch == '/') {
+      if (f != 8) return false;
+      --r;
+      f = 0;
+      continue;
+    }
+    if (ch >= '1' && ch <= '8') {
+      f += ch - '0';
+      if (f > 8) return false;
+      continue;
+    }
+    int pc = 0;
+    const char lc = (char)(ch | 32);
+    const int col = (ch >= 'a' && ch <= 'z') ? BLACK : WHITE;
+    switch (lc) {
+      case 'p': pc = PAWN; break;
+      case 'n': pc = KNIGHT; break;
+      case 'b': pc = BISHOP; break;
+      case 'r': pc = ROOK; break;
+      case 'q': pc = QUEEN; break;
+      case 'k': pc = KING; break;
+      default: return false;
+    }
+    if ((ch < 'A' || ch > 'Z') && (ch < 'a' || ch > 'z')) return false;
+    if (r < 0 || f > 7) return false;
+    put(b, r * 8 + f, make_piece_d(col, pc));
+    ++f;
+  }
+  if (r != 0 || f != 8) return false;
+  len = next_token(text, p, end, st);
+  if (len != 1 || (text[st] != 'w' && text[st] != 'b')) return false;
+  b.stm = text[st] == 'w' ? WHITE : BLACK;
+  if (__popcll(b.bt[KING] & b.bc[WHITE]) != 1 || __popcll(b.bt[KING] & b.bc[BLACK]) != 1) return false;
+  uint32_t cst;
+  const int clen = next_token(text, p, end, cst);
+  if (clen > 0 && !(clen == 1 && text[cst] == '-')) {
+    for (uint32_t i = cst; i < cst + (uint32_t)clen; ++i) {
+      const char ch = text[i];
+      const int col = (ch >= 'a' && ch <= 'z') ? BLACK : WHITE;
+      const char lc = (char)(ch | 32);
+      const int back = col == WHITE ? 0 : 56;
+      const int k = king_sq(b, col);
+      const int rook = make_piece_d(col, ROOK);
+      int rsq = -1, side = -1;
+      if ((k & 56) != back) continue;  // as the host: ignored before the character is checked
+      if (lc == 'k') {
+        side = 0;
+      } else if (lc == 'q') {
+        side = 1;
+      } else if (lc >= 'a' && lc <= 'h') {
+        side = 2;
+      } else {
+        return false;
+      }
+      if (side == 0) {
+        for (int x = back + 7; x > k; --x)
+          if (piece_at(b, x) == rook) { rsq = x; break; }
+      } else if (side == 1) {
+        for (int x = back; x < k; ++x)
+          if (piece_at(b, x) == rook) { rsq = x; break; }
+      } else {
+        rsq = back + (lc - 'a');
+        if (piece_at(b, rsq) != rook) rsq = -1;
+        side = rsq > k ? 0 : 1;
+        b.c960 = 1;
+      }
+      if (rsq >= 0) b.cr[col][side] = (int8_t)rsq;
+    }
+  }
+  for (int col = 0; col < 2; ++col) {
+    const int k = king_sq(b, col);
+    for (int side = 0; side < 2; ++side) {
+      const int rsq = b.cr[col][side];
+      if (rsq < 0) continue;
+      if ((k & 7) != 4 || ((rsq & 7) != (side == 0 ? 7 : 0))) b.c960 = 1;
+    }
+  }
+  uint32_t est;
+  const int elen = next_token(text, p, end, est);
+  if (elen == 2 && text[est] >= 'a' && text[est] <= 'h' && text[est + 1] >= '1' && text[est + 1] <= '8')
+    b.ep = (int8_t)((text[est + 1] - '1') * 8 + (text[est] - 'a'));
+  return true;
+}
+
+// parse_uci (board.cpp): the legal move whose UCI text, in Chess960
+// (king-takes-rook) or, for standard positions, standard castling notation,
+// equals the token.
+__device__ bool match_uci(const DBoard& b, const char* tok, int len, DMove& out) {
+  if (len != 4 && len != 5) return false;
+  auto sqr = [&](int i) -> int {
+    const char f = tok[i], r = tok[i + 1];
+    return (f >= 'a' && f <= 'h' && r >= '1' && r <= '8') ? (r - '1') * 8 + (f - 'a') : -1;
+  };
+  const int from = sqr(0), to = sqr(2);
+  if (from < 0 || to < 0) return false;
+  int promo = 0;
+  if (len == 5) {
+    switch (tok[4]) {
+      case 'n': promo = KNIGHT; break;
+      case 'b': promo = BISHOP; break;
+      case 'r': promo = ROOK; break;
+      case 'q': promo = QUEEN; break;
+      case 'k': promo = KING; break;
+      case 'p': promo = PAWN; break;
+      default: return false;
+    }
+  }
+  bool found = false;
+  for_each_legal(b, [&](const DMove& m) -> bool {
+    if (m.from != from || m.promo != promo) return true;
+    const bool hit = m.to == to || (m.castle && !b.c960 && to == (m.from & 56) + (m.to > m.from ? 6 : 2));
+    if (hit) {
+      out = m;
+      found = true;
+    }
+    return !hit;
+  });
+  return found;
+}
+
+// ---- kernels ----
+// text layout of game g: FEN in [fen_off[g], mv_off[g]), moves in [mv_off[g], fen_off[g + 1]).
+__global__ void count_plies_kernel(const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
+                                   const uint32_t* __restrict__ mv_off, uint32_t ngames, uint32_t* __restrict__ plies) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngames) return;
+  plies[g] = 1u + (uint32_t)count_tokens(text, mv_off[g], fen_off[g + 1]);
+}
+
+__device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t game, uint32_t ply) {
+  if (atomicCAS(&err[0], 0u, code) == 0u) {
+    err[1] = game;
+    err[2] = ply;
+  }
+}
+
+// One thread per game: parse, replay, write the position (and, for the
+// children pass, the full state) of every ply.
+__global__ void replay_kernel(const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
+                              const uint32_t* __restrict__ mv_off, uint32_t ngames,
+                              const uint32_t* __restrict__ ply_off, fnnue_pos* __restrict__ out,
+                              DBoard* __restrict__ states, uint32_t* __restrict__ err) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngames) return;
+  DBoard b;
+  if (!parse_fen(text, fen_off[g], mv_off[g], b)) {
+    latch(err, kBuildErrFen, g, 0);
+    return;
+  }
+  uint32_t o = ply_off[g];
+  if (out) out[o] = pack(b);
+  if (states) states[o] = b;
+  uint32_t p = mv_off[g], st;
+  const uint32_t end = fen_off[g + 1];
+  uint32_t ply = 0;
+  int len;
+  while ((len = next_token(text, p, end, st)) > 0) {
+    ++ply;
+    DMove m;
+    if (!match_uci(b, text + st, len, m)) {
+      latch(err, kBuildErrMove, g, ply);
+      return;
+    }
+    do_move(b, m);
+    ++o;
+    if (out) out[o] = pack(b);
+    if (states) states[o] = b;
+  }
+}
+
+__global__ void count_children_kernel(const DBoard* __restrict__ states, uint32_t n, uint32_t* __restrict__ cnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DBoard b = states[i];
+  uint32_t c = 0;
+  for_each_legal(b, [&](const DMove&) -> bool {
+    ++c;
+    return true;
+  });
+  cnt[i] = 1u + c;
+}
+
+__global__ void write_children_kernel(const DBoard* __restrict__ states, uint32_t n, const uint32_t* __restrict__ off,
+                                      fnnue_pos* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DBoard b = states[i];
+  uint32_t o = off[i];
+  out[o++] = pack(b);
+  for_each_legal(b, [&](const DMove& m) -> bool {
+    DBoard c = b;
+    do_move(c, m);
+    out[o++] = pack(c);
+    return true;
+  });
+}
+
+template <int D>
+__device__ uint64_t perft_dev(const DBoard& b) {
+  uint64_t n = 0;
+  for_each_legal(b, [&](const DMove& m) -> bool {
+    if constexpr (D <= 1) {
+      ++n;
+    } else {
+      DBoard c = b;
+      do_move(c, m);
+      n += perft_dev<D - 1>(c);
+    }
+    return true;
+  });
+  return n;
+}
+
+template <int D>
+__global__ void perft_kernel(const DBoard* __restrict__ states, uint32_t n, unsigned long long* __restrict__ total) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  atomicAdd(total, (unsigned long long)perft_dev<D>(states[i]));
+}
+
+// Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub).
+hipError_t exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s) {
+  size_t tmp_bytes = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, (int)n + 1, s);
+  if (e != hipSuccess) return e;
+  void* tmp = nullptr;
+  if ((e = hipMalloc(&tmp, tmp_bytes)) != hipSuccess) return e;
+  e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)n + 1, s);
+  const hipError_t e2 = hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  return e != hipSuccess ? e : e2;
+}
+
+}  // namespace
+
+DBoard to_dboard(const Board& h) {
+  DBoard b{};
+  b.bc[0] = h.byColor[0];
+  b.bc[1] = h.byColor[1];
+  for (int t = 0; t < 7; ++t) b.bt[t] = t ? h.byType[t] : 0;
+  for (int c = 0; c < 2; ++c)
+    for (int side = 0; side < 2; ++side) b.cr[c][side] = (int8_t)h.castle_rook[c][side];
+  b.ep = (int8_t)h.ep;
+  b.stm = (uint8_t)h.stm;
+  b.c960 = h.chess960 ? 1 : 0;
+  return b;
+}
+
+BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                               uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
+                               size_t off_cap, hipStream_t s) {
+  BuildResult R;
+  auto fail = [&](hipError_t e) {
+    R.hip = e;
+    return R;
+  };
+  hipError_t e;
+  uint32_t *plies = nullptr, *ply_off = nullptr, *err = nullptr, *cnt = nullptr, *coff = nullptr;
+  DBoard* states = nullptr;
+  struct Free {
+    std::vector<void*> p;
+    ~Free() {
+      for (void* x : p) (void)hipFree(x);
+    }
+  } F;
+  auto alloc = [&](void** p, size_t bytes) {
+    hipError_t a = hipMalloc(p, bytes ? bytes : 4);
+    if (a == hipSuccess) F.p.push_back(*p);
+    return a;
+  };
+  if ((e = alloc((void**)&plies, (size_t)(ngames + 1) * 4)) != hipSuccess) return fail(e);
+  if ((e = alloc((void**)&ply_off, (size_t)(ngames + 1) * 4)) != hipSuccess) return fail(e);
+  if ((e = alloc((void**)&err, 16)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(err, 0, 16, s)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(plies + ngames, 0, 4, s)) != hipSuccess) return fail(e);
+  const uint32_t bs = 64;
+  hipLaunchKernelGGL(count_plies_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
+                     ngames, plies);
+  if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+  if ((e = exclusive_scan(plies, ply_off, ngames, s)) != hipSuccess) return fail(e);
+  uint32_t total_plies = 0;
+  if ((e = hipMemcpy(&total_plies, ply_off + ngames, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
+  if (!children) {
+    R.n_out = total_plies;
+    R.n_groups = ngames;
+    if (cap < total_plies || off_cap < (size_t)ngames + 1 || !d_out || !d_group_off) {
+      R.capacity = true;
+      return R;
+    }
+    hipLaunchKernelGGL(replay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
+                       ngames, ply_off, d_out, (DBoard*)nullptr, err);
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(d_group_off, ply_off, (size_t)(ngames + 1) * 4, hipMemcpyDeviceToDevice, s)) !=
+        hipSuccess)
+      return fail(e);
+  } else {
+    if ((e = alloc((void**)&states, (size_t)total_plies * sizeof(DBoard))) != hipSuccess) return fail(e);
+    if ((e = alloc((void**)&cnt, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
+    if ((e = alloc((void**)&coff, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
+    hipLaunchKernelGGL(replay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
+                       ngames, ply_off, (fnnue_pos*)nullptr, states, err);
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    uint32_t herr[4];
+    if ((e = hipMemcpyAsync(herr, err, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
+    if (herr[0]) {
+      R.err_code = herr[0];
+      R.err_game = herr[1];
+      R.err_ply = herr[2];
+      return R;
+    }
+    if ((e = hipMemsetAsync(cnt + total_plies, 0, 4, s)) != hipSuccess) return fail(e);
+    hipLaunchKernelGGL(count_children_kernel, dim3((total_plies + bs - 1) / bs), dim3(bs), 0, s, states,
+                       total_plies, cnt);
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = exclusive_scan(cnt, coff, total_plies, s)) != hipSuccess) return fail(e);
+    uint32_t total = 0;
+    if ((e = hipMemcpy(&total, coff + total_plies, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
+    R.n_out = total;
+    R.n_groups = total_plies;
+    if (cap < total || off_cap < (size_t)total_plies + 1 || !d_out || !d_group_off) {
+      R.capacity = true;
+      return R;
+    }
+    hipLaunchKernelGGL(write_children_kernel, dim3((total_plies + bs - 1) / bs), dim3(bs), 0, s, states,
+                       total_plies, coff, d_out);
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(d_group_off, coff, (size_t)(total_plies + 1) * 4, hipMemcpyDeviceToDevice, s)) !=
+        hipSuccess)
+      return fail(e);
+  }
+  uint32_t herr[4];
+  if ((e = hipMemcpyAsync(herr, err, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
+  R.err_code = herr[0];
+  R.err_game = herr[1];
+  R.err_ply = herr[2];
+  return R;
+}
+
+hipError_t perft_device(const std::vector<DBoard>& frontier, int depth, uint64_t* nodes) {
+  *nodes = 0;
+  if (frontier.empty()) return hipSuccess;
+  if (depth < 1 || depth > 3) return hipErrorInvalidValue;
+  DBoard* d = nullptr;
+  unsigned long long* tot = nullptr;
+  hipError_t e = hipMalloc(&d, frontier.size() * sizeof(DBoard));
+  if (e != hipSuccess) return e;
+  if ((e = hipMalloc(&tot, 8)) == hipSuccess && (e = hipMemset(tot, 0, 8)) == hipSuccess &&
+      (e = hipMemcpy(d, frontier.data(), frontier.size() * sizeof(DBoard), hipMemcpyHostToDevice)) == hipSuccess) {
+    const uint32_t n = (uint32_t)frontier.size(), bs = 64;
+    if (depth == 1) hipLaunchKernelGGL(perft_kernel<1>, dim3((n + bs - 1) / bs), dim3(bs), 0, 0, d, n, tot);
+    else if (depth == 2) hipLaunchKernelGGL(perft_kernel<2>, dim3((n + bs - 1) / bs), dim3(bs), 0, 0, d, n, tot);
+    else hipLaunchKernelGGL(perft_kernel<3>, dim3((n + bs - 1) / bs), dim3(bs), 0, 0, d, n, tot);
+    if ((e = hipGetLastError()) == hipSuccess) {
+      unsigned long long h = 0;
+      e = hipMemcpy(&h, tot, 8, hipMemcpyDeviceToHost);
+      *nodes = h;
+    }
+  }
+  (void)hipFree(d);
+  if (tot) (void)hipFree(tot);
+  return e;
+}
+
+}  // namespace fnnue

@@ -18,6 +18,7 @@
 
 #include "../../include/fnnue.h"
 #include "board.h"
+#include "builder.h"
 #include "kernels.h"
 #include "net.h"
 
@@ -721,4 +722,123 @@ int fnnue_selftest_mfma(int device) {
   return FNNUE_OK;
 }
 
+
+int fnnue_build_batch_device(fnnue_ctx* ctx, const char* d_text, const uint32_t* d_fen_off,
+                             const uint32_t* d_moves_off, size_t ngames, int mode, fnnue_pos* d_out, size_t cap,
+                             uint32_t* d_off, size_t off_cap, size_t* n_out, size_t* n_groups, void* stream) {
+  if (!ctx || !n_out || !n_groups) return fail(FNNUE_E_ARG, "null argument");
+  if (mode != FNNUE_PLAYOUT_PLIES && mode != FNNUE_PLAYOUT_CHILDREN) return fail(FNNUE_E_ARG, "bad build mode");
+  *n_out = *n_groups = 0;
+  if (ngames == 0) return FNNUE_OK;
+  if (!d_text || !d_fen_off || !d_moves_off) return fail(FNNUE_E_ARG, "null buffer");
+  if (ngames > (1u << 26)) return fail(FNNUE_E_ARG, "too many games");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const BuildResult R = build_batch_device(d_text, d_fen_off, d_moves_off, (uint32_t)ngames,
+                                           mode == FNNUE_PLAYOUT_CHILDREN, d_out, cap, d_off, off_cap, s);
+  if (R.hip != hipSuccess) return hip_fail(R.hip, "device batch builder");
+  *n_out = R.n_out;
+  *n_groups = R.n_groups;
+  if (R.err_code == kBuildErrFen)
+    return fail(FNNUE_E_FEN, "unparsable FEN in game " + std::to_string(R.err_game));
+  if (R.err_code == kBuildErrMove)
+    return fail(FNNUE_E_MOVE, "illegal move at ply " + std::to_string(R.err_ply) + " of game " +
+                                  std::to_string(R.err_game));
+  if (R.capacity) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  return FNNUE_OK;
+}
+
+int fnnue_build_batch(fnnue_ctx* ctx, const char* text, size_t text_len, const uint32_t* fen_off,
+                      const uint32_t* moves_off, size_t ngames, int mode, fnnue_pos* out, size_t cap, uint32_t* off,
+                      size_t off_cap, size_t* n_out, size_t* n_groups) {
+  if (!ctx || !n_out || !n_groups || (ngames && (!text || !fen_off || !moves_off)))
+    return fail(FNNUE_E_ARG, "null argument");
+  *n_out = *n_groups = 0;
+  if (ngames == 0) return FNNUE_OK;
+  if (fen_off[ngames] > text_len) return fail(FNNUE_E_ARG, "offsets exceed the text");
+  for (size_t i = 0; i < ngames; ++i)
+    if (fen_off[i] > moves_off[i] || moves_off[i] > fen_off[i + 1]) return fail(FNNUE_E_ARG, "offsets out of order");
+  DeviceGuard g(ctx->device);
+  struct Bufs {
+    std::vector<void*> p;
+    ~Bufs() {
+      for (void* x : p) (void)hipFree(x);
+    }
+  } B;
+  auto dalloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 4) != hipSuccess) return nullptr;
+    B.p.push_back(p);
+    return p;
+  };
+  char* d_text = (char*)dalloc(text_len);
+  uint32_t* d_fo = (uint32_t*)dalloc((ngames + 1) * 4);
+  uint32_t* d_mo = (uint32_t*)dalloc(ngames * 4);
+  if (!d_text || !d_fo || !d_mo) return fail(FNNUE_E_OOM, "device allocation (builder input)");
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(d_text, text, text_len, hipMemcpyHostToDevice, s), "H2D");
+  HIP_TRY(hipMemcpyAsync(d_fo, fen_off, (ngames + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
+  HIP_TRY(hipMemcpyAsync(d_mo, moves_off, ngames * 4, hipMemcpyHostToDevice, s), "H2D");
+  int rc = fnnue_build_batch_device(ctx, d_text, d_fo, d_mo, ngames, mode, nullptr, 0, nullptr, 0, n_out, n_groups, s);
+  if (rc != FNNUE_E_CAPACITY) return rc;  // sizing pass: always "too small" with no outputs
+  if (!out || !off || cap < *n_out || off_cap < *n_groups + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  fnnue_pos* d_out = (fnnue_pos*)dalloc(*n_out * sizeof(fnnue_pos));
+  uint32_t* d_off = (uint32_t*)dalloc((*n_groups + 1) * 4);
+  if (!d_out || !d_off) return fail(FNNUE_E_OOM, "device allocation (builder output)");
+  rc = fnnue_build_batch_device(ctx, d_text, d_fo, d_mo, ngames, mode, d_out, *n_out, d_off, *n_groups + 1, n_out,
+                                n_groups, s);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, d_out, *n_out * sizeof(fnnue_pos), hipMemcpyDeviceToHost, s), "D2H");
+  HIP_TRY(hipMemcpyAsync(off, d_off, (*n_groups + 1) * 4, hipMemcpyDeviceToHost, s), "D2H");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  return FNNUE_OK;
+}
+
+int fnnue_perft_device(fnnue_ctx* ctx, const char* fen, int depth, uint64_t* nodes) {
+  if (!ctx || !fen || !nodes || depth < 1 || depth > 8) return fail(FNNUE_E_ARG, "bad argument");
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  // host expands the first depth - 3 levels, the device counts the rest
+  std::vector<Board> level{b}, next;
+  std::vector<Move> ms;
+  for (int d = depth; d > 3; --d) {
+    next.clear();
+    for (const Board& x : level) {
+      x.legal_moves(ms);
+      for (const Move& m : ms) {
+        Board c = x;
+        c.do_move(m);
+        next.push_back(c);
+      }
+    }
+    level.swap(next);
+  }
+  std::vector<DBoard> frontier;
+  frontier.reserve(level.size());
+  for (const Board& x : level) frontier.push_back(to_dboard(x));
+  DeviceGuard g(ctx->device);
+  HIP_TRY(perft_device(frontier, std::min(depth, 3), nodes), "device perft");
+  return FNNUE_OK;
+}
+
+int fnnue_random_game(uint64_t seed, const char* fen, uint32_t plies, char* moves, size_t cap, size_t* len) {
+  if (!fen || !len) return fail(FNNUE_E_ARG, "null argument");
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  uint64_t st = seed;
+  std::string out;
+  for (uint32_t i = 0; i < plies; ++i) {
+    Move m;
+    if (!b.random_legal_move(st, m)) break;
+    if (!out.empty()) out += ' ';
+    out += b.uci(m, b.chess960);
+    b.do_move(m);
+  }
+  *len = out.size();
+  if (!moves || cap < out.size() + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  std::memcpy(moves, out.c_str(), out.size() + 1);
+  return FNNUE_OK;
+}
 }  // extern "C"

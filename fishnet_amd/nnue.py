@@ -135,6 +135,26 @@ class Evaluator:
     def check(self) -> None:
         N.check(N.lib.fnnue_ctx_check(self._h))
 
+    # Device-side batch builder (fnnue_build_batch): games = [(fen, "uci uci ..."), ...].
+    def build_batch(self, games, mode: int = N.PLAYOUT_PLIES) -> tuple[np.ndarray, np.ndarray]:
+        text, fen_off, mv_off = pack_games(games)
+        n, g = C.c_size_t(), C.c_size_t()
+        rc = N.lib.fnnue_build_batch(self._h, text, len(text), N.ptr(fen_off), N.ptr(mv_off), len(games), mode,
+                                     None, 0, None, 0, C.byref(n), C.byref(g))
+        if rc != -10:  # FNNUE_E_CAPACITY reports the sizes; anything else is final
+            N.check(rc)
+            return N.positions_array(0), np.zeros(1, dtype=np.uint32)
+        out = N.positions_array(n.value)
+        off = np.zeros(g.value + 1, dtype=np.uint32)
+        N.check(N.lib.fnnue_build_batch(self._h, text, len(text), N.ptr(fen_off), N.ptr(mv_off), len(games), mode,
+                                        N.ptr(out), len(out), N.ptr(off), len(off), C.byref(n), C.byref(g)))
+        return out[: n.value], off[: g.value + 1]
+
+    def perft_device(self, fen: str, depth: int) -> int:
+        nodes = C.c_uint64()
+        N.check(N.lib.fnnue_perft_device(self._h, fen.encode(), depth, C.byref(nodes)))
+        return nodes.value
+
     def set_ft_impl(self, impl: int) -> None:
         """FT_SLICED (default, LDS-stationary tiles) or FT_GATHER (per-position row gather)."""
         N.check(N.lib.fnnue_ctx_set_ft_impl(self._h, impl))
@@ -210,6 +230,30 @@ def random_playouts(seed: int, count: int, min_plies: int = 0, max_plies: int = 
     if mode == N.PLAYOUT_FINAL:
         return out[: n.value]
     return out[: n.value], off[: g.value + 1]
+
+
+def pack_games(games) -> tuple[bytes, np.ndarray, np.ndarray]:
+    """[(fen, moves)] -> the builder's text layout: FEN g in [fen_off[g], mv_off[g]),
+    its moves in [mv_off[g], fen_off[g + 1])."""
+    parts, fen_off, mv_off, pos = [], [], [], 0
+    for fen, moves in games:
+        if not isinstance(moves, str):
+            moves = " ".join(moves)
+        f, m = fen.encode(), b" " + moves.encode()
+        fen_off.append(pos)
+        mv_off.append(pos + len(f))
+        parts += [f, m]
+        pos += len(f) + len(m)
+    fen_off.append(pos)
+    return b"".join(parts), np.array(fen_off, dtype=np.uint32), np.array(mv_off, dtype=np.uint32)
+
+
+def random_game(seed: int, fen: str, plies: int) -> str:
+    """Up to `plies` random legal moves from `fen` as space-separated UCI (test inputs)."""
+    n = C.c_size_t()
+    buf = C.create_string_buffer(8 * plies + 16)
+    N.check(N.lib.fnnue_random_game(seed, fen.encode(), plies, buf, len(buf), C.byref(n)))
+    return buf.value.decode()
 
 
 def perft(fen: str, depth: int) -> int:

@@ -161,6 +161,38 @@ int fnnue_random_playouts(uint64_t seed, size_t count, uint32_t min_plies, uint3
 /* perft node count (board-code self test against published known answers). */
 int fnnue_perft(const char *fen, int depth, uint64_t *nodes);
 
+/* ---- batch building on the device ----
+ * The batch expansion of fnnue_game_positions / fnnue_game_children for a
+ * whole batch at once, on the GPU (FEN parse, UCI replay with Chess960
+ * castling / en passant / promotion, legal children): replaces the
+ * per-game host loop of IncomingBatch::from_acquired ([ref] src/queue.rs:
+ * 518-627; wire format src/api.rs:293-309) and produces the positions where
+ * the evaluator reads them.  Results are record for record those of the host
+ * builder.
+ * d_text (device memory): game g's FEN in [fen_off[g], moves_off[g]) and its
+ * space-separated UCI moves in [moves_off[g], fen_off[g + 1]); d_fen_off has
+ * ngames + 1 entries, d_moves_off ngames (both device memory).
+ *  FNNUE_PLAYOUT_PLIES: every ply of every game; group g = game g (CHAIN).
+ *  FNNUE_PLAYOUT_CHILDREN: one STAR group per ply: the ply, then its legal
+ *    children in generation order.
+ * Synchronous on `stream` (sizes are read back).  *n_out / *n_groups are set
+ * even when the call fails with FNNUE_E_CAPACITY (retry with bigger buffers);
+ * FNNUE_E_FEN / FNNUE_E_MOVE name the first failing game and ply. */
+int fnnue_build_batch_device(fnnue_ctx *ctx, const char *d_text, const uint32_t *d_fen_off,
+                             const uint32_t *d_moves_off, size_t ngames, int mode, fnnue_pos *d_out, size_t cap,
+                             uint32_t *d_off, size_t off_cap, size_t *n_out, size_t *n_groups, void *stream);
+/* Same with host buffers (staged through the ctx's stream). */
+int fnnue_build_batch(fnnue_ctx *ctx, const char *text, size_t text_len, const uint32_t *fen_off,
+                      const uint32_t *moves_off, size_t ngames, int mode, fnnue_pos *out, size_t cap, uint32_t *off,
+                      size_t off_cap, size_t *n_out, size_t *n_groups);
+/* perft on the device (depth <= 3 per thread; shallower levels expanded on
+ * the host): pins the device move generator on published counts. */
+int fnnue_perft_device(fnnue_ctx *ctx, const char *fen, int depth, uint64_t *nodes);
+/* A random legal game from `fen`: up to `plies` uniformly random legal moves
+ * (splitmix64 seed), space-separated UCI (Chess960 notation when the position
+ * needs it), NUL-terminated; *len = string length.  Test-input generator. */
+int fnnue_random_game(uint64_t seed, const char *fen, uint32_t plies, char *moves, size_t cap, size_t *len);
+
 /* ---- diagnostics ----
  * Runs the int8 MFMA operand-layout self test on `device`; 0 if the hardware
  * layout matches the kernels' assumption. */
