@@ -156,9 +156,9 @@ __device__ __noinline__ bool legal(const DBoard& b, const DMove& m) {
 // Legal moves in the order of Board::pseudo_moves + is_legal (board.cpp):
 // own pieces by square; a pawn's push (promotions Q, R, B, N), double push,
 // captures by square, en passant; then castling king side, queen side.
-// f(move) returns false to stop early.
+// f(move) returns false to stop early.  Only pieces on `from_mask` move.
 template <class F>
-__device__ void for_each_legal(const DBoard& b, F&& f) {
+__device__ void for_each_legal(const DBoard& b, F&& f, uint64_t from_mask = ~0ull) {
   const int us = b.stm, them = us ^ 1;
   const uint64_t occ = b.bc[0] | b.bc[1], own = b.bc[us], opp = b.bc[them];
   const int up = us == WHITE ? 8 : -8;
@@ -167,7 +167,7 @@ __device__ void for_each_legal(const DBoard& b, F&& f) {
     const DMove m{from, to, promo, castle};
     return !legal(b, m) || f(m);
   };
-  for (uint64_t pcs = own; pcs; pcs &= pcs - 1) {
+  for (uint64_t pcs = own & from_mask; pcs; pcs &= pcs - 1) {
     const int s = lsb(pcs);
     const uint64_t sm = 1ull << s;
     if (b.bt[PAWN] & sm) {
@@ -202,7 +202,7 @@ __device__ void for_each_legal(const DBoard& b, F&& f) {
   }
   const int ksq = king_sq(b, us);
   const int back = us == WHITE ? 0 : 56;
-  if (ksq < 0 || (ksq & 56) != back) return;
+  if (ksq < 0 || (ksq & 56) != back || !((from_mask >> ksq) & 1)) return;
   for (int side = 0; side < 2; ++side) {
     const int rsq = b.cr[us][side];
     if (rsq < 0 || piece_at(b, rsq) != make_piece_d(us, ROOK)) continue;
@@ -383,7 +383,7 @@ __device__ bool match_uci(const DBoard& b, const char* tok, int len, DMove& out)
       found = true;
     }
     return !hit;
-  });
+  }, 1ull << from);  // only the moving piece's moves: same order, same first match
   return found;
 }
 
