@@ -71,6 +71,7 @@ struct fnnue_ctx {
   size_t stage_cap = 0, off_cap = 0;
   int ft_impl = FNNUE_FT_SLICED;
   SlicedPlan plan{};
+  SegPlan seg{};                // incremental sliced path for groups (allocated on first use)
   bool timing = false;
   std::vector<std::array<hipEvent_t, 3>> evpool;  // per timed launch: before ft, between, after stack
   size_t evused = 0;
@@ -99,7 +100,8 @@ void ctx_destroy(fnnue_ctx* c) {
   for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off,
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
                   (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm,
-                  (void*)c->plan.psqt_part})
+                  (void*)c->plan.psqt_part, (void*)c->seg.ref, (void*)c->seg.cref, c->seg.dtmp, c->seg.drec,
+                  (void*)c->seg.ipos, (void*)c->seg.len, c->seg.items, c->seg.scan_temp})
     if (p) (void)hipFree(p);
   delete c;
 }
@@ -224,6 +226,19 @@ int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
     c->evpool.push_back(trio);
   }
   *out = &c->evpool[c->evused++];
+  return FNNUE_OK;
+}
+
+int ensure_seg(fnnue_ctx* c) {
+  SegPlan& G = c->seg;
+  if (G.ref) return FNNUE_OK;
+  const size_t n2 = 2 * (size_t)kChunk;
+  G.scan_temp_bytes = seg_scan_temp_bytes(kChunk);
+  if (hipMalloc(&G.ref, (n2 + 1) * 4) != hipSuccess || hipMalloc(&G.cref, (n2 + 1) * 4) != hipSuccess ||
+      hipMalloc(&G.dtmp, n2 * 16) != hipSuccess || hipMalloc(&G.drec, n2 * 16) != hipSuccess ||
+      hipMalloc(&G.ipos, n2 * 4) != hipSuccess || hipMalloc(&G.len, n2 * 4) != hipSuccess ||
+      hipMalloc(&G.items, n2 * 16) != hipSuccess || hipMalloc(&G.scan_temp, G.scan_temp_bytes + 16) != hipSuccess)
+    return fail(FNNUE_E_OOM, "device allocation (segment plan)");
   return FNNUE_OK;
 }
 
@@ -454,6 +469,10 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
   if (!d_pos || !d_off || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (ctx->ft_impl == FNNUE_FT_SLICED) {
+    const int rc = ensure_seg(ctx);
+    if (rc) return rc;
+  }
   std::vector<uint32_t> off(ngroups + 1);
   HIP_TRY(hipMemcpyAsync(off.data(), d_off, off.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpy");
   HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
@@ -471,10 +490,17 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
     int rc = next_events(ctx, &ev);
     if (rc) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
-    HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs, ctx->x,
-                             d_psqt + base, ctx->bucket, ctx->err, s),
-            "ft_groups launch");
-    rc = run_chunk_tail(ctx, m, d_positional + base, s, ev);
+    if (ctx->ft_impl == FNNUE_FT_SLICED) {
+      HIP_TRY(launch_ft_segments(ctx->hd, d_pos + base, m, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs,
+                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s),
+              "ft_segments launch");
+      rc = run_chunk_tail(ctx, m, d_positional + base, s, ev, nullptr, ctx->plan.psqt_part, d_psqt + base);
+    } else {
+      HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs, ctx->x,
+                               d_psqt + base, ctx->bucket, ctx->err, s),
+              "ft_groups launch");
+      rc = run_chunk_tail(ctx, m, d_positional + base, s, ev);
+    }
     if (rc) return rc;
     gb = ge;
   }

@@ -1,0 +1,483 @@
+// ft_segments.hip — incremental feature transformer on LDS tiles, for grouped
+// positions (CHAIN: a game's plies in order; STAR: a parent and its
+// children), BASELINE configs 3 and 4.
+//
+// Upstream Stockfish updates an accumulator incrementally along the
+// StateInfo chain (nnue_feature_transformer.h update_accumulator: subtract the
+// removed feature rows, add the added ones) and refreshes it when the
+// perspective's own king moved (HalfKAv2_hm::requires_refresh).  While a
+// perspective's own king stays put its features all live in one king block,
+// i.e. in one LDS tile of the sliced layout (ft_sliced.hip).  So a *segment*
+// = a refresh position and the positions derived from it without another
+// refresh (CHAIN: the following plies; STAR: the parent's children) is
+// processed by the 8 lanes of one item inside the (king block, slice)
+// workgroup that holds the tile: the refresh position sums its full feature
+// list, every further position applies <= 2 removed and <= 2 added rows to
+// the previous accumulator (CHAIN) or to the parent's (STAR).  int16 add/sub
+// wrap is a group, so results equal a refresh bit for bit.
+//
+// Plan (all on the device, per chunk of positions):
+//   seg_delta     per (position, perspective): refresh flag or the delta
+//                 record {slot, half, bucket, 2 removed, 2 added rows}
+//   scan          exclusive scan of refresh flags -> item index per refresh
+//   seg_items     item k -> its root position; segment length 1
+//   seg_members   delta records placed at root + rank (a segment's plies
+//                 contiguous), segment lengths (atomicMax)
+//   seg_count / plan_scan / seg_scatter   counting sort of items by
+//                 (king block, length), unit table, full lists (write_rows)
+//   ft_segments   (unit, slice) workgroups, XCD-aware, tile in LDS
+// then stack_kernel over x / bucket / psqt_part in position order.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "sliced_common.h"
+
+namespace fnnue {
+
+namespace {
+
+constexpr uint32_t kSlotMask = 0xFFFFFF;  // record x: slot | half << 24 | bucket << 25
+
+// Which group position i (chunk-relative) belongs to: first position of it.
+__device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
+                                                uint32_t i) {
+  uint32_t lo = 0, hi = ngroups;  // off[lo] - base <= i < off[hi] - base
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (off[mid] - base <= i) lo = mid;
+    else hi = mid;
+  }
+  return off[lo] - base;
+}
+
+__device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int ksq, int kb) {
+  return 16u * (uint32_t)(make_index(persp, s, pc, ksq) - kRowsPerBlock * kb);
+}
+
+__global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                                        const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                        uint32_t base, int star, uint32_t* __restrict__ ref,
+                                                        uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
+                                                        uint32_t* __restrict__ err) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const LaneBoard B = lane_decode(pos + i);
+  if (!B.ok) {
+    // no item, no accumulator; counted as a refresh so that STAR ranks skip it
+    bucket[i] = 0xFF;
+    ref[i] = ref[n + i] = 1;
+    atomicOr(err, 1u);
+    return;
+  }
+  const uint32_t bk = (uint32_t)(B.cnt - 1) >> 2;
+  bucket[i] = (uint8_t)bk;
+  const uint32_t first = group_first(off, ngroups, base, i);
+  const bool has_base = i > first;
+  LaneBoard A;
+  bool base_ok = false;
+  uint64_t changed = 0;
+  if (has_base) {
+    A = lane_decode(pos + (star ? first : i - 1));
+    base_ok = A.ok;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      changed |= (uint64_t)nibble_bits(~zero_nibbles(A.w[k] ^ B.w[k]) & 0x88888888u) << (8 * k);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ksq = c ? B.bk : B.wk;
+    bool refresh = !base_ok || (c ? A.bk : A.wk) != ksq || __popcll(changed) > 4;
+    uint32_t rem[2] = {kNoEntry, kNoEntry}, add[2] = {kNoEntry, kNoEntry};
+    if (!refresh) {
+      const int kb = king_block(c, ksq);
+      int nr = 0, na = 0;
+      for (uint64_t m = changed; m; m &= m - 1) {
+        const int s = __builtin_ctzll(m);
+        const int was = nibble_at(A.w, s), now = nibble_at(B.w, s);
+        if (was) {
+          if (nr < 2) rem[nr] = feature_entry(c, s, was, ksq, kb);
+          ++nr;
+        }
+        if (now) {
+          if (na < 2) add[na] = feature_entry(c, s, now, ksq, kb);
+          ++na;
+        }
+      }
+      refresh = nr > 2 || na > 2;  // never for a legal move; arbitrary groups refresh
+    }
+    ref[c * n + i] = refresh ? 1u : 0u;
+    if (!refresh) {
+      const uint32_t half = B.stm == c ? 0u : 1u;
+      dtmp[c * n + i] = make_uint4(i | half << 24 | bk << 25, rem[0] | rem[1] << 16, add[0] | add[1] << 16, 0u);
+    }
+  }
+}
+
+// cref = exclusive scan of ref[0 .. 2n): refresh (c, i) is item cref[c*n+i].
+__global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint8_t* __restrict__ bucket,
+                                                        const uint32_t* __restrict__ ref,
+                                                        const uint32_t* __restrict__ cref, uint32_t* __restrict__ ipos,
+                                                        uint32_t* __restrict__ len) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n || !ref[j] || bucket[j % n] == 0xFF) return;
+  ipos[cref[j]] = j % n;
+  len[j] = 1;
+}
+
+__global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint32_t* __restrict__ off,
+                                                          uint32_t ngroups, uint32_t base, int star,
+                                                          const uint8_t* __restrict__ bucket,
+                                                          const uint32_t* __restrict__ ref,
+                                                          const uint32_t* __restrict__ cref,
+                                                          const uint32_t* __restrict__ ipos,
+                                                          const uint4* __restrict__ dtmp, uint4* __restrict__ drec,
+                                                          uint32_t* __restrict__ len) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n || ref[j]) return;
+  const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+  if (bucket[i] == 0xFF) return;  // invalid position: no accumulator
+  uint32_t r, rank;
+  if (star) {
+    r = group_first(off, ngroups, base, i);  // the parent: a refresh item of this perspective
+    rank = (i - r) - (cref[j] - cref[c * n + r + 1]);
+  } else {
+    r = ipos[cref[j] - 1];  // the last refresh of this perspective before i (same game)
+    rank = i - r;
+  }
+  drec[c * n + r + rank] = dtmp[j];
+  atomicMax(&len[c * n + r], rank + 1);
+}
+
+__device__ __forceinline__ uint32_t seg_key(const LaneBoard& b, int c, uint32_t L) {
+  return (uint32_t)king_block(c, c ? b.bk : b.wk) * 33u + min(L, 33u) - 1u;
+}
+
+__global__ __launch_bounds__(1024) void seg_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                                         const uint32_t* __restrict__ ref,
+                                                         const uint32_t* __restrict__ len,
+                                                         uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t h[kItemBins];
+  for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < 2 * n; j += gridDim.x * blockDim.x) {
+    if (!ref[j] || !len[j]) continue;  // len = 0: invalid position
+    const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+    atomicAdd(&h[seg_key(lane_decode(pos + i), (int)c, len[j])], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kItemBins; i += blockDim.x)
+    if (h[i]) atomicAdd(&ctr[kCnt + i], h[i]);
+}
+
+// Sorted item record: {root | half << 24 | bucket << 25, length, perspective,
+// piece count}; full feature list of the root as in the sliced plan.
+__global__ __launch_bounds__(1024) void seg_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                                           const uint32_t* __restrict__ ref,
+                                                           const uint32_t* __restrict__ len,
+                                                           uint32_t* __restrict__ ctr, uint4* __restrict__ items,
+                                                           uint16_t* __restrict__ flist) {
+  __shared__ uint32_t lcnt[kItemBins];
+  __shared__ uint32_t lbase[kItemBins];
+  for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) lcnt[i] = 0;
+  __syncthreads();
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = j < 2 * n && ref[j] && len[j];
+  const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+  LaneBoard b;
+  uint32_t key = 0, rk = 0, L = 0;
+  if (live) {
+    b = lane_decode(pos + i);
+    L = len[j];
+    key = seg_key(b, (int)c, L);
+    rk = atomicAdd(&lcnt[key], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < kItemBins; k += blockDim.x)
+    lbase[k] = lcnt[k] ? atomicAdd(&ctr[kCur + k], lcnt[k]) : 0;
+  __syncthreads();
+  if (!live) return;
+  const uint32_t slot = lbase[key] + rk;
+  const uint32_t half = b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(b.cnt - 1) >> 2;
+  items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)b.cnt);
+  write_rows(b, (int)c, c ? b.bk : b.wk, slot, ctr, flist);
+}
+
+struct SegFetch {
+  uint4 rec;
+  uint2 lst;
+};
+
+__device__ __forceinline__ SegFetch fetch_seg(__amdgpu_buffer_rsrc_t items, __amdgpu_buffer_rsrc_t flist,
+                                              int pass_base, int last, int lane, int it_in_wave) {
+  SegFetch f;
+  const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(items, (uint32_t)min(pass_base + it_in_wave, last) * 16u, 0, 0);
+  f.rec = make_uint4(r.x, r.y, r.z, r.w);
+  const uint32_t li = (uint32_t)min(pass_base + (lane >> 3), last);
+  const u32x2 l = __builtin_amdgcn_raw_buffer_load_b64(flist, li * 64u + 8u * (uint32_t)(lane & 7), 0, 0);
+  f.lst = make_uint2(l.x, l.y);
+  return f;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
+// One delta position: cur = base -/+ the removed / added rows of record d.
+__device__ __forceinline__ void apply_delta(const char* lbase, const uint4& d, u16x4 b_lo, u16x4 b_hi, u16x4& lo,
+                                            u16x4& hi) {
+  const u32x4 r0 = *row_addr(lbase, d.y, 0), r1 = *row_addr(lbase, d.y, 1);
+  const u32x4 a0 = *row_addr(lbase, d.z, 0), a1 = *row_addr(lbase, d.z, 1);
+  auto lo2 = [](const u32x4& v) { return __builtin_bit_cast(u16x4, __builtin_shufflevector(v, v, 0, 1)); };
+  auto hi2 = [](const u32x4& v) { return __builtin_bit_cast(u16x4, __builtin_shufflevector(v, v, 2, 3)); };
+  lo = b_lo - lo2(r0) - lo2(r1) + lo2(a0) + lo2(a1);
+  hi = b_hi - hi2(r0) - hi2(r1) + hi2(a0) + hi2(a1);
+}
+
+__device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4& d, int q) {
+  auto p = [&](uint32_t e) { return ptile[(e >> 4) * kPsqtBuckets + q]; };
+  return (int32_t)((uint32_t)p(d.z & 0xFFFFu) + (uint32_t)p(d.z >> 16) - (uint32_t)p(d.y & 0xFFFFu) -
+                   (uint32_t)p(d.y >> 16));
+}
+
+// One pass = 8 segment items per wave.  Refresh position: as slice_pass
+// (ft_sliced.hip) but the PSQT sum keeps all 8 buckets, one per lane q of the
+// item, because the bucket changes along a segment.  Then the wave walks the
+// longest segment of the pass; finished items turn their rows into the zero
+// row and their stores out of range (dropped).
+template <int HD, bool kStar>
+__device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
+                                         int q, uint32_t n, const char* lbase, u16x4 b_lo, u16x4 b_hi, int krow,
+                                         const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
+                                         __amdgpu_buffer_rsrc_t x_rsrc, __amdgpu_buffer_rsrc_t drec_rsrc) {
+  const uint4 rec = f.rec;
+  const uint32_t maxn = wave_max_u32(rec.w), maxL = wave_max_u32(rec.y);
+  lb[lane] = f.lst;
+  uint32_t e[16];
+  const uint4* my = reinterpret_cast<const uint4*>(lb) + 4 * it_in_wave;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint4 v = my[m];
+    e[4 * m] = v.x;
+    e[4 * m + 1] = v.y;
+    e[4 * m + 2] = v.z;
+    e[4 * m + 3] = v.w;
+  }
+  u16x4 lo = b_lo, hi = b_hi;
+  switch ((maxn + 2) >> 2) {
+    case 1: rows_pipelined<1>(e, lbase, lo, hi); break;
+    case 2: rows_pipelined<2>(e, lbase, lo, hi); break;
+    case 3: rows_pipelined<3>(e, lbase, lo, hi); break;
+    case 4: rows_pipelined<4>(e, lbase, lo, hi); break;
+    case 5: rows_pipelined<5>(e, lbase, lo, hi); break;
+    case 6: rows_pipelined<6>(e, lbase, lo, hi); break;
+    case 7: rows_pipelined<7>(e, lbase, lo, hi); break;
+    case 8: rows_pipelined<8>(e, lbase, lo, hi); break;
+    default: break;
+  }
+  const uint32_t col = 32 * s + 4 * q;
+  __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc,
+                                        ((rec.x & kSlotMask) * 2 + ((rec.x >> 24) & 1)) * (HD / 2) + col, 0, 0);
+  int32_t p = 0;
+  if (s == 0) {
+    const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
+    uint32_t acc = (uint32_t)ptile[krow * kPsqtBuckets + q];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) acc += (uint32_t)ptile[(ent[j] >> 4) * kPsqtBuckets + q];
+    p = (int32_t)acc;
+  }
+  auto psqt_off = [&](uint32_t x, bool live) {
+    return (s == 0 && live && (int)(x >> 25) == q) ? ((x & kSlotMask) * 2 + ((x >> 24) & 1)) * 4u : kDroppedOffset;
+  };
+  __builtin_amdgcn_raw_buffer_store_b32(p, psqt_rsrc, psqt_off(rec.x, true), 0, 0);
+  if (maxL <= 1) return;
+  // Delta positions k = 1 .. maxL-1: records at drec[c*n + root + k], fetched
+  // two ahead; a finished item (k >= L) reads past the buffer (zeros) and is
+  // masked to the zero row.
+  const uint32_t rbase = (rec.z * n + (rec.x & kSlotMask)) * 16u;
+  auto fetch = [&](uint32_t k) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drec_rsrc, k < rec.y ? rbase + 16u * k : kDroppedOffset, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  };
+  uint4 d1 = fetch(1), d2 = fetch(2);
+  u16x4 blo = lo, bhi = hi;
+  int32_t pb = p;
+  for (uint32_t k = 1; k < maxL; ++k) {
+    uint4 d = d1;
+    d1 = d2;
+    d2 = fetch(k + 2);
+    const bool live = k < rec.y;
+    if (!live) d = make_uint4(0u, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
+    apply_delta(lbase, d, blo, bhi, lo, hi);
+    const uint32_t xo = live ? ((d.x & kSlotMask) * 2 + ((d.x >> 24) & 1)) * (HD / 2) + col : kDroppedOffset;
+    __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
+    int32_t pc = 0;
+    if (s == 0) pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta(ptile, d, q));
+    __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, psqt_off(d.x, live), 0, 0);
+    if constexpr (!kStar) {
+      blo = lo;
+      bhi = hi;
+      pb = pc;
+    }
+  }
+}
+
+template <int HD, bool kStar>
+__global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restrict__ tiles,
+                                                           const int16_t* __restrict__ ftb,
+                                                           const uint32_t* __restrict__ ctr,
+                                                           const int4* __restrict__ units,
+                                                           const uint4* __restrict__ items,
+                                                           const uint16_t* __restrict__ flist,
+                                                           const uint4* __restrict__ drec, uint32_t n,
+                                                           const int32_t* __restrict__ psqw,
+                                                           int32_t* __restrict__ psqt_part,
+                                                           uint8_t* __restrict__ x) {
+  constexpr int S = HD / 64;
+  __shared__ uint4 img[kTileU4];
+  __shared__ int32_t ptile[kTileRows * kPsqtBuckets];
+  __shared__ uint2 lbuf[16][64];
+  const uint32_t w = blockIdx.x;
+  const uint32_t j = w >> 3;
+  const uint32_t unit = (j / S) * 8 + (w & 7);
+  const int s = (int)(j % S);
+  if (unit >= ctr[kNUnits]) return;
+  const int4 u = units[unit];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int it_in_wave, q;
+  lane_item(lane, it_in_wave, q);
+  constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
+  constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
+  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
+  uint4 t[kTileLoads];
+#pragma unroll
+  for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
+  uint4 pt[2];
+  const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
+  if (s == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
+  }
+  u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
+  u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+  const int krow = king_row(u.x);
+  const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
+  uint2* lb = lbuf[wv];
+  // Buffer ranges are this launch's exact extents (x: n rows of HD bytes,
+  // < 2^31; psqt_part: 2n words; drec: 2n records): finished items store and
+  // load at kDroppedOffset, past num_records, so the hardware drops them, and
+  // no record can reach beyond the launch's rows.
+  const __amdgpu_buffer_rsrc_t psqt_rsrc = __builtin_amdgcn_make_buffer_rsrc(psqt_part, 0, (int)(8 * n), kBufferFlags);
+  const __amdgpu_buffer_rsrc_t x_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(x, 0, (int)min((uint64_t)n * HD, (uint64_t)kBufferRange), kBufferFlags);
+  const __amdgpu_buffer_rsrc_t items_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(items), 0, kBufferAll, kBufferFlags);
+  const __amdgpu_buffer_rsrc_t flist_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(flist), 0, kBufferAll, kBufferFlags);
+  const __amdgpu_buffer_rsrc_t drec_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n), kBufferFlags);
+  const int last = u.z - 1;
+  int base = u.y + wv * 8;
+  SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
+#pragma unroll
+  for (int k = 0; k < kTileLoads; ++k)
+    if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
+  if (s == 0) {
+    uint4* pdst = reinterpret_cast<uint4*>(ptile);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = (int)threadIdx.x + 1024 * k;
+      if (i < kPtileU4) pdst[i] = i < kPtileRealU4 ? pt[k] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  {
+    const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
+    const u32x2 klo = __builtin_shufflevector(kv, kv, 0, 1), khi = __builtin_shufflevector(kv, kv, 2, 3);
+    b_lo += __builtin_bit_cast(u16x4, klo);
+    b_hi += __builtin_bit_cast(u16x4, khi);
+  }
+  while (base < u.z) {
+    const SegFetch cur = fa;
+    fa = fetch_seg(items_rsrc, flist_rsrc, base + 128, last, lane, it_in_wave);
+    seg_pass<HD, kStar>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc,
+                        drec_rsrc);
+    base += 128;
+  }
+}
+
+template <int HD>
+hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& net, uint32_t n, bool star,
+                         uint8_t* x, uint32_t max_units, hipStream_t stream) {
+  constexpr int S = HD / 64;
+  const uint32_t groups = (max_units + 7) / 8;
+  if (star)
+    hipLaunchKernelGGL((ft_segments_kernel<HD, true>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+                       (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, (const uint4*)G.items, P.flist,
+                       (const uint4*)G.drec, n, net.psqt_w, P.psqt_part, x);
+  else
+    hipLaunchKernelGGL((ft_segments_kernel<HD, false>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+                       (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, (const uint4*)G.items, P.flist,
+                       (const uint4*)G.drec, n, net.psqt_w, P.psqt_part, x);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+size_t seg_scan_temp_bytes(uint32_t chunk) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         (int)(2 * chunk + 1));
+  return b;
+}
+
+#define FNNUE_HD_DISPATCH(hd, CALL) \
+  switch (hd) {                     \
+    case 128: return CALL(128);     \
+    case 256: return CALL(256);     \
+    case 512: return CALL(512);     \
+    case 1024: return CALL(1024);   \
+    case 2048: return CALL(2048);   \
+    default: return hipErrorInvalidValue; \
+  }
+
+hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
+                              uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
+                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const bool star = mode == FNNUE_GROUP_STAR;
+  hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return e;
+  // ref[2n] is followed by one zero word so the scan yields cref[2n] = item count
+  if ((e = hipMemsetAsync(G.ref + 2 * (size_t)n, 0, 4, stream)) != hipSuccess) return e;
+  const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
+  hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, off, ngroups, base, star ? 1 : 0, G.ref,
+                     (uint4*)G.dtmp, bucket, err);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  size_t tb = G.scan_temp_bytes;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(G.scan_temp, tb, G.ref, G.cref, (int)(2 * n + 1), stream)) != hipSuccess)
+    return e;
+  if ((e = hipMemsetAsync(G.len, 0, 2 * (size_t)n * 4, stream)) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_items_kernel, dim3(g2), dim3(bs), 0, stream, n, bucket, G.ref, G.cref, G.ipos, G.len);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_members_kernel, dim3(g2), dim3(bs), 0, stream, n, off, ngroups, base, star ? 1 : 0, bucket,
+                     G.ref, G.cref, G.ipos, (const uint4*)G.dtmp, (uint4*)G.drec, G.len);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  uint32_t cb = (2 * n + 1023) / 1024;
+  if (cb > 256) cb = 256;
+  hipLaunchKernelGGL(seg_count_kernel, dim3(cb), dim3(1024), 0, stream, pos, n, G.ref, G.len, P.ctr);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_scatter_kernel, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.ref, G.len,
+                     P.ctr, (uint4*)G.items, P.flist);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint32_t mu = sliced_max_units(n);
+#define CALL(H) ft_segments_t<H>(G, P, net, n, star, x, mu, stream)
+  FNNUE_HD_DISPATCH(hd, CALL)
+#undef CALL
+}
+
+}  // namespace fnnue

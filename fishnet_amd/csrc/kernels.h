@@ -67,6 +67,26 @@ hipError_t launch_sliced_ft(uint32_t hd, uint32_t n, const NetPtrs& net, const S
 hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
                             uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream);
 
+// Incremental FT on LDS tiles for CHAIN / STAR groups (ft_segments.hip).
+// Uses the sliced plan's tiles, counters, unit table, lists and psqt_part;
+// writes x[i], bucket[i], psqt_part[2i + half] in position order, then run
+// launch_stack with perm = null and psqt_part.
+struct SegPlan {
+  uint32_t* ref;      // [2 * chunk + 1] refresh flags per (perspective, position)
+  uint32_t* cref;     // [2 * chunk + 1] exclusive scan of ref
+  void* dtmp;         // uint4 [2 * chunk] delta records by position
+  void* drec;         // uint4 [2 * chunk] delta records at root + rank
+  uint32_t* ipos;     // [2 * chunk] item -> root position
+  uint32_t* len;      // [2 * chunk] segment length at the root
+  void* items;        // uint4 [2 * chunk] sorted item records
+  void* scan_temp;
+  size_t scan_temp_bytes;
+};
+size_t seg_scan_temp_bytes(uint32_t chunk);
+hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
+                              uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
+                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream);
+
 // MFMA operand-layout self test: returns number of mismatching outputs in *bad.
 hipError_t run_mfma_selftest(int* bad);
 

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
     if (psqt_part && row_ok && g == 1) {
       // upstream transform(): (psqtAcc[stm][b] - psqtAcc[~stm][b]) / 2, int32 wrap then C division
       const int v = bk == 0xFF ? 0 : (int)((uint32_t)psqt_part[2 * prow] - (uint32_t)psqt_part[2 * prow + 1]) / 2;
-      psqt[perm[prow]] = v;
+      psqt[perm ? perm[prow] : prow] = v;
     }
     uint32_t bmask = 0;
 #pragma unroll

@@ -1,0 +1,376 @@
+// sliced_common.h — device pieces shared by the LDS-stationary feature
+// transformer kernels (ft_sliced.hip: independent positions; ft_segments.hip:
+// incremental segments of games): tile layout, lane-per-position decode,
+// feature lists, the plan scan, transform and the pipelined row reads.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "kernels.h"
+#include "net.h"
+
+namespace fnnue {
+namespace {
+
+constexpr int kRowsPerBlock = 704;            // PS_NB: rows per king block
+constexpr int kTileRows = kRowsPerBlock + 1;  // + one zero row
+constexpr int kNoRow = kRowsPerBlock;         // the zero row
+// Tile layout, in HBM and in LDS: 8 planes q (16-byte column chunks), each
+// 705 rows x 16 B padded to kPlaneBytes = 11296 = 32 (mod 256).  Chunk q of row
+// r then sits in banks 8q + 4r + [0,4) (mod 64): one row's 8 chunks are
+// conflict-free and rows of opposite parity use complementary banks.
+constexpr int kPlaneBytes = 11296;
+constexpr int kPlaneU4 = kPlaneBytes / 16;    // 706
+constexpr int kTileU4 = 8 * kPlaneU4;         // 5648 x 16 B = 90,368 B
+// Feature-list entries are 16*row (u16), the byte offset of the row inside a
+// plane: ft_slices forms the LDS address base_q + entry with one SDWA add.
+constexpr uint32_t kNoEntry = 16 * kNoRow;
+// Row (within king block kb) of the own-king feature: KingBuckets is a
+// bijection between kb and the oriented king square o on files e-h, and the
+// king plane is 10 (upstream half_ka_v2_hm.h), so every item of kb has it.
+__host__ __device__ constexpr int king_row(int kb) { return 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3)); }
+constexpr int kItemBins = 32 * 33;            // key = kb * 33 + n
+constexpr int kPosBins = 9;                   // bucket 0..7, 8 = invalid
+constexpr int kBins = kItemBins + kPosBins;
+#ifndef PLAN_WG
+#define PLAN_WG 1024
+#endif
+constexpr int kScatterPositions = PLAN_WG;    // positions per plan_scatter workgroup (one per lane)
+
+// Counter block layout (uint32 words).
+constexpr int kCnt = 0, kOff = kBins, kCur = 2 * kBins, kNUnits = 3 * kBins;
+
+// ds_read_b128 services a wave in four 16-lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32).  Give each group exactly two items of 8 lanes so
+// a group touches two 128-B rows (at most a 2-way bank conflict).
+__device__ __forceinline__ void lane_item(int lane, int& item, int& q) {
+  const int l = lane & 31, hi = (lane >> 5) * 4;
+  if (l < 4) { item = 0; q = l; }
+  else if (l < 12) { item = 2; q = l - 4; }
+  else if (l < 16) { item = 0; q = l - 8; }
+  else if (l < 20) { item = 3; q = l - 16; }
+  else if (l < 28) { item = 1; q = l - 20; }
+  else { item = 3; q = l - 24; }
+  item += hi;
+}
+
+// ---------------------------------------------------------------------------
+// Lane-per-position decode of a packed position (64 nibbles in 8 words) with
+// SWAR nibble tests: the plan kernels touch every position once, so they
+// decode 64 positions per wave instead of one.
+struct LaneBoard {
+  uint32_t w[8];
+  uint64_t occ;
+  int stm, wk, bk, cnt;
+  bool ok;
+};
+
+// Bit 4k+3 set iff nibble k of y is zero.
+__device__ __forceinline__ uint32_t zero_nibbles(uint32_t y) {
+  return ~(((y & 0x77777777u) + 0x77777777u) | y) & 0x88888888u;
+}
+
+// Compresses bits 3, 7, ..., 31 into an 8-bit mask.
+__device__ __forceinline__ uint32_t nibble_bits(uint32_t z) {
+  uint32_t m = z >> 3;
+  m = (m | (m >> 3)) & 0x03030303u;
+  m = (m | (m >> 6)) & 0x000F000Fu;
+  return (m | (m >> 12)) & 0xFFu;
+}
+
+__device__ __forceinline__ LaneBoard lane_decode(const fnnue_pos* p) {
+  LaneBoard b;
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b.w[i] = pw[i];
+  b.stm = (int)(pw[8] & 0xFF);
+  b.occ = 0;
+  int nwk = 0, nbk = 0;
+  uint32_t bad = 0;
+  b.wk = b.bk = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = b.w[i];
+    b.occ |= (uint64_t)nibble_bits(~zero_nibbles(w) & 0x88888888u) << (8 * i);
+    const uint32_t kw = zero_nibbles(w ^ 0x66666666u), kb = zero_nibbles(w ^ 0xEEEEEEEEu);
+    nwk += __popc(kw);
+    nbk += __popc(kb);
+    if (kw) b.wk = 8 * i + (__builtin_ctz(kw) >> 2);
+    if (kb) b.bk = 8 * i + (__builtin_ctz(kb) >> 2);
+    bad |= zero_nibbles(w ^ 0x77777777u) | zero_nibbles(w ^ 0x88888888u) | zero_nibbles(~w);
+  }
+  b.cnt = __popcll(b.occ);
+  b.ok = !bad && nwk == 1 && nbk == 1 && b.cnt <= 32 && b.stm <= 1;
+  return b;
+}
+
+__device__ __forceinline__ int nibble_at(const uint32_t (&w)[8], int s) {
+  const int i = s >> 3;
+  const uint32_t a = (i & 1) ? w[1] : w[0], c = (i & 1) ? w[3] : w[2];
+  const uint32_t e = (i & 1) ? w[5] : w[4], g = (i & 1) ? w[7] : w[6];
+  const uint32_t lo = (i & 2) ? c : a, hi = (i & 2) ? g : e;
+  return (int)((((i & 4) ? hi : lo) >> (4 * (s & 7))) & 15u);
+}
+
+// One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ ctr, int4* __restrict__ units,
+                                                         uint32_t unit_items) {
+  __shared__ uint32_t s[kBins];
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  // Exclusive scan of the item bins and, separately, of the position bins.
+  constexpr int per = (kBins + 1023) / 1024;
+  uint32_t local[per];
+  uint32_t sum = 0;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    local[k] = (i < kItemBins) ? ctr[kCnt + i] : 0;
+    sum += local[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i < kItemBins) s[i] = run;
+    run += local[k];
+  }
+  if (t == 0) {
+    uint32_t r = 0;
+    for (int b = 0; b < kPosBins; ++b) {
+      s[kItemBins + b] = r;
+      r += ctr[kCnt + kItemBins + b];
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < kBins; i += 1024) {
+    ctr[kOff + i] = s[i];
+    ctr[kCur + i] = s[i];
+  }
+  if (t < 32) {
+    // Unit table: each king block's item range in chunks of <= unit_items;
+    // lane kb counts its block's units, a wave prefix sum places them.
+    const int kb = t;
+    const uint32_t b = s[kb * 33];
+    const uint32_t e = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
+    const uint32_t mine = (e - b + unit_items - 1) / unit_items;
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 32);
+      if (kb >= o) incl += v;
+    }
+    uint32_t nu = incl - mine;
+    for (uint32_t c = b; c < e; c += unit_items) units[nu++] = make_int4(kb, (int)c, (int)min(e, c + unit_items), 0);
+    if (kb == 31) ctr[kNUnits] = incl;
+  }
+}
+
+// Writes item `it`'s 32 feature-list entries (rows relative to its king block,
+// padded with the zero row): every piece except the perspective's own king,
+// whose row is the same for the whole king block (king_row) and is added to
+// the bias once per workgroup instead of once per item.  ft_slices pairs items 2k and 2k+1 of a pass on
+// one ds_read_b128 lane group; a 128-B tile row r lies in bank half r & 1, so
+// even-position items list their even rows first and odd-position items their
+// odd rows first: the pair then mostly reads opposite bank halves.  A row's
+// parity is (square ^ mirror) & 1 (orient() flips files when the king is on
+// files a-d), and the sum is order-independent.
+__device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ksq, uint32_t it,
+                                           const uint32_t* __restrict__ ctr, uint16_t* __restrict__ flist) {
+  const int kbc = king_block(persp, ksq);
+  const uint32_t pp = (it - ctr[kOff + kbc * 33]) & 1;
+  const uint32_t mirror = (ksq & 7) < 4 ? 1u : 0u;
+  constexpr uint64_t kEvenFiles = 0x5555555555555555ull;
+  const uint64_t occ = b.occ & ~(1ull << ksq);  // own king: folded into the bias (king_row)
+  uint64_t first = occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
+  uint64_t second = occ & ~first;
+  uint32_t E[16];
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t a = kNoEntry;
+    if (first | second) {
+      uint64_t& m = first ? first : second;
+      const int sq = __builtin_ctzll(m);
+      m &= m - 1;
+      a = 16u * (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
+    }
+    if (k & 1) E[k >> 1] |= a << 16;
+    else E[k >> 1] = a;
+  }
+  uint4* dst = reinterpret_cast<uint4*>(flist + (size_t)it * 32);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dst[k] = make_uint4(E[4 * k], E[4 * k + 1], E[4 * k + 2], E[4 * k + 3]);
+}
+
+// Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
+// x 705 rows x 8 entries per row.  Single source of truth for the allocation
+// (sliced_tiles_bytes) and the relayout kernel's extent.
+__host__ __device__ constexpr size_t tile_uint4_count(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileU4; }
+
+// ---------------------------------------------------------------------------
+// Tile image: tile(kb, s)[q][r] (16 B) = {ft_w[kb*704+r][32s+4q .. +3],
+// ft_w[kb*704+r][HD/2+32s+4q .. +3]}; r = 704 is the zero row, r = 705 padding.
+template <int HD>
+__global__ __launch_bounds__(256) void relayout_kernel(const int16_t* __restrict__ ftw, uint4* __restrict__ tiles) {
+  constexpr int S = HD / 64;
+  constexpr size_t total = tile_uint4_count(HD);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i % kPlaneU4);
+    const size_t t = i / kPlaneU4;
+    const int q = (int)(t & 7);
+    const size_t ks = t >> 3;
+    const int s = (int)(ks % S), kb = (int)(ks / S);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < kRowsPerBlock) {
+      const int16_t* row = ftw + (size_t)(kb * kRowsPerBlock + r) * HD;
+      const uint2 lo = *reinterpret_cast<const uint2*>(row + 32 * s + 4 * q);
+      const uint2 hi = *reinterpret_cast<const uint2*>(row + HD / 2 + 32 * s + 4 * q);
+      v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+    }
+    tiles[i] = v;
+  }
+}
+
+// Raw buffer resources: num_records = 2^31 - 1 bytes, so any offset >= 2^31
+// fails the bounds check and the store is dropped.  Word 3 = the gfx9-family
+// raw-buffer format (32-bit data format, no swizzle).
+constexpr int kBufferRange = 0x7FFFFFFF;
+constexpr int kBufferFlags = 0x00020000;
+constexpr int kBufferAll = -1;  // num_records = 2^32 - 1: no bounds check in practice
+constexpr uint32_t kDroppedOffset = 0x80000000u;
+
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// out byte k = (clamp(lo_k, 0, 127) * clamp(hi_k, 0, 127)) >> 7 (upstream
+// transform).  The doubled product (< 2^15) holds that value in its high byte,
+// so one v_perm_b32 packs the four bytes.
+__device__ __forceinline__ uint32_t transform4(u16x4 lo, u16x4 hi) {
+  const s16x4 zero = (s16x4)0, top = (s16x4)127;
+  const s16x4 a = __builtin_elementwise_min(__builtin_elementwise_max((s16x4)lo, zero), top);
+  const s16x4 b = __builtin_elementwise_min(__builtin_elementwise_max((s16x4)hi, zero), top);
+  const u16x4 pr = ((u16x4)a * (u16x4)b) << (u16x4)1;
+  const u32x2 w = __builtin_bit_cast(u32x2, pr);
+  return __builtin_amdgcn_perm(w.y, w.x, 0x07050301u);
+}
+
+// One pass's fetch from HBM/L2: this lane's item record, and 8 bytes of the
+// pass's feature lists (lane l: entries 4(l&7) .. +3 of pass item l>>3), so
+// each list byte is fetched once per slice; the lists are then spread to the
+// 8 lanes of each item through a per-wave LDS buffer.  Indices are clamped into
+// the unit so the loads are unconditional (hipcc then counts vmcnt instead of
+// draining it); a clamped lane repeats the unit's last item.
+struct PassFetch {
+  uint32_t rec;
+  uint2 lst;
+};
+__device__ __forceinline__ PassFetch fetch_pass(__amdgpu_buffer_rsrc_t items, __amdgpu_buffer_rsrc_t flist,
+                                                int pass_base, int last, int lane, int it_in_wave) {
+  PassFetch f;
+  f.rec = __builtin_amdgcn_raw_buffer_load_b32(items, (uint32_t)min(pass_base + it_in_wave, last) * 4u, 0, 0);
+  const uint32_t li = (uint32_t)min(pass_base + (lane >> 3), last);
+#ifdef FT_EXP_NO_LIST
+  f.lst = make_uint2(f.rec & 0x70, f.rec & 0x30);
+#else
+  const u32x2 l = __builtin_amdgcn_raw_buffer_load_b64(flist, li * 64u + 8u * (uint32_t)(lane & 7), 0, 0);
+  f.lst = make_uint2(l.x, l.y);
+#endif
+  return f;
+}
+
+// Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
+// 16-byte chunk q of the row).
+
+// LDS byte address of this lane's chunk of the row named by the low / high u16
+// entry of `word`: base (= plane q) + entry; hipcc emits one v_add_u32_sdwa.
+__device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word, int t) {
+  const uint32_t entry = (t & 1) ? (word >> 16) : (word & 0xFFFFu);
+  return static_cast<const u32x4*>(__builtin_assume_aligned(base + entry, 16));
+}
+
+template <int G>
+__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], const char* base, u32x4 (&v)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    v[t] = *row_addr(base, e[2 * G + (t >> 1)], t);
+#ifdef FT_EXP_DUPREAD
+    const u32x4 extra = *(row_addr(base, e[2 * G + (t >> 1)], t) + 1);
+    uint32_t sink;
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(sink) : "v"(extra.x), "v"(extra.y));
+#endif
+  }
+}
+
+__device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4& hi) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    // Swizzles go through named temporaries: __builtin_bit_cast of a swizzle
+    // lvalue (v.zw) reads from the vector's base address in this clang.
+    const u32x2 a = __builtin_shufflevector(v[t], v[t], 0, 1);
+    const u32x2 b = __builtin_shufflevector(v[t], v[t], 2, 3);
+    lo += __builtin_bit_cast(u16x4, a);
+#ifdef FT_EXP_EXTRAVALU
+    {
+      uint32_t sink;
+      asm volatile("v_xor_b32 %0, %1, %2" : "=v"(sink) : "v"(a.x), "v"(b.y));
+    }
+#endif
+#ifdef FT_EXP_DUPADD
+    {
+      uint32_t s0, s1, s2, s3;
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s0) : "v"(a.x), "v"(a.y));
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s1) : "v"(a.y), "v"(b.x));
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s2) : "v"(b.x), "v"(b.y));
+      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s3) : "v"(b.y), "v"(a.x));
+    }
+#endif
+#ifndef FT_EXP_LO_ONLY
+    hi += __builtin_bit_cast(u16x4, b);
+#endif
+  }
+}
+
+#ifndef FT_DEPTH
+#define FT_DEPTH 3
+#endif
+constexpr int kDepth = FT_DEPTH;  // row groups (of 4) in flight per wave
+
+// NG groups of 4 rows, kDepth groups in flight, no branches: the LDS queue
+// stays fed and hipcc can count lgkmcnt instead of draining it.
+template <int NG, int G = 0>
+__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kDepth][4],
+                                          u16x4& lo, u16x4& hi) {
+  if constexpr (G < NG) {
+    accum_rows(v[G % kDepth], lo, hi);
+    if constexpr (G + kDepth < NG) issue_rows<G + kDepth>(e, base, v[G % kDepth]);
+    rows_step<NG, G + 1>(e, base, v, lo, hi);
+  }
+}
+
+template <int NG, int G = 0>
+__device__ __forceinline__ void rows_issue_head(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kDepth][4]) {
+  if constexpr (G < NG && G < kDepth) {
+    issue_rows<G>(e, base, v[G]);
+    rows_issue_head<NG, G + 1>(e, base, v);
+  }
+}
+
+template <int NG>
+__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
+#ifndef FT_EXP_NO_ROWS
+  u32x4 v[kDepth][4];
+  rows_issue_head<NG>(e, base, v);
+  rows_step<NG>(e, base, v, lo, hi);
+#endif
+}
+
+}  // namespace
+}  // namespace fnnue

@@ -199,8 +199,11 @@ int fnnue_random_game(uint64_t seed, const char *fen, uint32_t plies, char *move
 int fnnue_selftest_mfma(int device);
 /* Feature-transformer implementation for fnnue_eval_positions*:
  *  FNNUE_FT_SLICED (default): LDS-stationary weight tiles, positions planned
- *    and sorted on the device.
- *  FNNUE_FT_GATHER: one wave per position gathering rows from L2/HBM.
+ *    and sorted on the device; for fnnue_eval_groups*, the
+ *    incremental updates run on the same tiles (segments of positions that
+ *    share the perspective's king square).
+ *  FNNUE_FT_GATHER: one wave per position (groups: per group) gathering rows
+ *    from L2/HBM.
  * Both are bit-identical; the environment variable FNNUE_FT_IMPL=gather|sliced
  * sets the default for new contexts. */
 #define FNNUE_FT_SLICED 0

@@ -204,3 +204,73 @@ def test_image_broadcast_path(ev_cache):
     a, b = ev.eval_positions(pos), ev2.eval_positions(pos)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     ev2.close()
+
+
+@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (6, 2048, 0), (3, 1024, N.SYNTH_WRAP)])
+def test_group_impls_agree(ev_cache, seed, hd, flags):
+    """Incremental groups: LDS-tile segments (sliced, default) == per-group
+    gather kernel == oracle, for CHAIN games and STAR children."""
+    ev, on = ev_cache(seed, hd, flags)
+    for mode, pm, count in ((N.GROUP_CHAIN, N.PLAYOUT_PLIES, 400), (N.GROUP_STAR, N.PLAYOUT_CHILDREN, 40)):
+        pos, off = F.random_playouts(seed + 20, count, mode=pm, threads=8)
+        res = []
+        for impl in (N.FT_SLICED, N.FT_GATHER):
+            ev.set_ft_impl(impl)
+            res.append(ev.eval_groups(pos, off, mode))
+        ev.set_ft_impl(N.FT_SLICED)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        for ps, po in res:
+            assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_groups_of_unrelated_positions(ev_cache):
+    """Groups need not be games: big diffs and king jumps refresh."""
+    ev, on = ev_cache()
+    pos = F.random_playouts(5, 3000, threads=8)
+    off = np.array([0, 1, 7, 500, 501, 2999, 3000], dtype=np.uint32)
+    for mode in (N.GROUP_CHAIN, N.GROUP_STAR):
+        ps, po = ev.eval_groups(pos, off, mode)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_groups_with_invalid_position(ev_cache):
+    """An invalid position fails the batch (host API) and never feeds a delta."""
+    ev, on = ev_cache()
+    pos, off = F.random_playouts(9, 30, mode=N.PLAYOUT_PLIES, threads=8)
+    bad = pos.copy()
+    bad[off[3] + 2, :32] = 0  # no kings
+    with pytest.raises(F.FnnueError) as e:
+        ev.eval_groups(bad, off, N.GROUP_CHAIN)
+    assert e.value.name == "FNNUE_E_POSITION"
+    ps, po = ev.eval_groups(pos, off, N.GROUP_CHAIN)  # ctx still usable
+    ops, opo, rc = on.eval_packed(pos, threads=8)
+    assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_groups_device_latched_invalid(ev_cache):
+    """Device entry point: invalid positions inside CHAIN/STAR groups give 0/0,
+    the rest stay exact (refresh after the hole), error latched."""
+    import torch
+    ev, on = ev_cache()
+    for mode, pm in ((N.GROUP_CHAIN, N.PLAYOUT_PLIES), (N.GROUP_STAR, N.PLAYOUT_CHILDREN)):
+        pos, off = F.random_playouts(10, 20, mode=pm, threads=8)
+        holes = [int(off[2]) + 1, int(off[5]), int(off[7]) + 3]
+        bad = pos.copy()
+        for h in holes:
+            bad[h, :32] = 0
+        dev = torch.device("cuda", 0)
+        d_pos = torch.from_numpy(bad).to(dev)
+        d_off = torch.from_numpy(off.astype(np.int32)).to(dev)
+        d_ps = torch.full((len(pos),), 77, dtype=torch.int32, device=dev)
+        d_po = torch.full((len(pos),), 77, dtype=torch.int32, device=dev)
+        ev.eval_groups_device(d_pos.data_ptr(), d_off.data_ptr(), len(off) - 1, len(pos), mode, d_ps.data_ptr(),
+                              d_po.data_ptr(), None)
+        with pytest.raises(F.FnnueError):
+            ev.check()
+        ps, po = d_ps.cpu().numpy(), d_po.cpu().numpy()
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        ok = np.ones(len(pos), dtype=bool)
+        ok[holes] = False
+        assert np.all(ps[~ok] == 0) and np.all(po[~ok] == 0)
+        assert np.array_equal(ps[ok], ops[ok]) and np.array_equal(po[ok], opo[ok])
