@@ -143,7 +143,7 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
   SlicedPlan& P = c->plan;
   if (hipMalloc(&P.tiles, sliced_tiles_bytes(hd)) != hipSuccess ||
       hipMalloc(&P.ctr, sliced_ctr_words() * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&P.units, (size_t)sliced_max_units(kChunk) * 16) != hipSuccess ||
+      hipMalloc(&P.units, (size_t)std::max(sliced_max_units(kChunk), seg_max_units(kChunk)) * 16) != hipSuccess ||
       hipMalloc(&P.items, (size_t)2 * kChunk * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&P.flist, (size_t)2 * kChunk * 32 * sizeof(uint16_t)) != hipSuccess ||
       hipMalloc(&P.perm, (size_t)kChunk * sizeof(uint32_t)) != hipSuccess ||

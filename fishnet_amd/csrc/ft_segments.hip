@@ -20,11 +20,13 @@
 //   seg_delta     per (position, perspective): refresh flag or the delta
 //                 record {slot, half, bucket, 2 removed, 2 added rows}
 //   scan          exclusive scan of refresh flags -> item index per refresh
-//   seg_items     item k -> its root position; segment length 1
+//   seg_items     item k -> its root position
+//   seg_len       segment length per refresh (next refresh / group parent)
 //   seg_members   delta records placed at root + rank (a segment's plies
-//                 contiguous), segment lengths (atomicMax)
+//                 contiguous)
 //   seg_count / plan_scan / seg_scatter   counting sort of items by
-//                 (king block, length), unit table, full lists (write_rows)
+//                 (king block, length bin), unit table cut at ~4096
+//                 positions, full lists (write_rows)
 //   ft_segments   (unit, slice) workgroups, XCD-aware, tile in LDS
 // then stack_kernel over x / bucket / psqt_part in position order.
 #include <hip/hip_runtime.h>
@@ -37,17 +39,23 @@ namespace fnnue {
 namespace {
 
 constexpr uint32_t kSlotMask = 0xFFFFFF;  // record x: slot | half << 24 | bucket << 25
+// A segment item is a whole run of positions walked serially, so units are
+// cut by positions (kSegUnitPlies, plan_scan_kernel) rather than by items.
 
-// Which group position i (chunk-relative) belongs to: first position of it.
-__device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
-                                                uint32_t i) {
+// The group of position i (chunk-relative): its first position and its end.
+__device__ __forceinline__ uint2 group_range(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
+                                             uint32_t i) {
   uint32_t lo = 0, hi = ngroups;  // off[lo] - base <= i < off[hi] - base
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (off[mid] - base <= i) lo = mid;
     else hi = mid;
   }
-  return off[lo] - base;
+  return make_uint2(off[lo] - base, off[lo + 1] - base);
+}
+__device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
+                                                uint32_t i) {
+  return group_range(off, ngroups, base, i).x;
 }
 
 __device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int ksq, int kb) {
@@ -113,15 +121,37 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
   }
 }
 
-// cref = exclusive scan of ref[0 .. 2n): refresh (c, i) is item cref[c*n+i].
-__global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint8_t* __restrict__ bucket,
-                                                        const uint32_t* __restrict__ ref,
-                                                        const uint32_t* __restrict__ cref, uint32_t* __restrict__ ipos,
-                                                        uint32_t* __restrict__ len) {
+// cref = exclusive scan of ref[0 .. 2n): refresh (c, i) is item cref[c*n+i]
+// (invalid positions count as refreshes without an item).
+__global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint32_t* __restrict__ ref,
+                                                        const uint32_t* __restrict__ cref,
+                                                        uint32_t* __restrict__ ipos) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2 * n || !ref[j] || bucket[j % n] == 0xFF) return;
-  ipos[cref[j]] = j % n;
-  len[j] = 1;
+  if (j < 2 * n && ref[j]) ipos[cref[j]] = j % n;
+}
+
+// Segment length at each valid refresh (0 elsewhere).  CHAIN: up to the next
+// refresh of the same perspective (the next item; groups start with one).
+// STAR: the group's parent owns its children that are not refreshes.
+__global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                      uint32_t base, int star, const uint8_t* __restrict__ bucket,
+                                                      const uint32_t* __restrict__ ref,
+                                                      const uint32_t* __restrict__ cref,
+                                                      const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= 2 * n) return;
+  const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+  uint32_t L = 0;
+  if (ref[j] && bucket[i] != 0xFF) {
+    if (star) {
+      const uint2 g = group_range(off, ngroups, base, i);
+      L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
+    } else {
+      const uint32_t k = cref[j];
+      L = (k + 1 < cref[(c + 1) * n] ? ipos[k + 1] : n) - i;
+    }
+  }
+  len[j] = L;
 }
 
 __global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint32_t* __restrict__ off,
@@ -130,12 +160,10 @@ __global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint
                                                           const uint32_t* __restrict__ ref,
                                                           const uint32_t* __restrict__ cref,
                                                           const uint32_t* __restrict__ ipos,
-                                                          const uint4* __restrict__ dtmp, uint4* __restrict__ drec,
-                                                          uint32_t* __restrict__ len) {
+                                                          const uint4* __restrict__ dtmp, uint4* __restrict__ drec) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= 2 * n || ref[j]) return;
   const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
-  if (bucket[i] == 0xFF) return;  // invalid position: no accumulator
   uint32_t r, rank;
   if (star) {
     r = group_first(off, ngroups, base, i);  // the parent: a refresh item of this perspective
@@ -145,11 +173,10 @@ __global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint
     rank = i - r;
   }
   drec[c * n + r + rank] = dtmp[j];
-  atomicMax(&len[c * n + r], rank + 1);
 }
 
 __device__ __forceinline__ uint32_t seg_key(const LaneBoard& b, int c, uint32_t L) {
-  return (uint32_t)king_block(c, c ? b.bk : b.wk) * 33u + min(L, 33u) - 1u;
+  return (uint32_t)king_block(c, c ? b.bk : b.wk) * 33u + seg_len_bin(L);
 }
 
 __global__ __launch_bounds__(1024) void seg_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
@@ -243,16 +270,18 @@ __device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4&
 
 // One pass = 8 segment items per wave.  Refresh position: as slice_pass
 // (ft_sliced.hip) but the PSQT sum keeps all 8 buckets, one per lane q of the
-// item, because the bucket changes along a segment.  Then the wave walks the
-// longest segment of the pass; finished items turn their rows into the zero
-// row and their stores out of range (dropped).
-template <int HD, bool kStar>
+// item, because the bucket changes along a segment (kPsqt: slice 0 only).
+// Then the wave walks the longest segment of the pass; finished items turn
+// their rows into the zero row and their stores out of range (dropped).
+template <int HD, bool kStar, bool kPsqt>
 __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
                                          int q, uint32_t n, const char* lbase, u16x4 b_lo, u16x4 b_hi, int krow,
                                          const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
-                                         __amdgpu_buffer_rsrc_t x_rsrc, __amdgpu_buffer_rsrc_t drec_rsrc) {
+                                         __amdgpu_buffer_rsrc_t x_rsrc, __amdgpu_buffer_rsrc_t drec_rsrc,
+                                         uint4* __restrict__ dbuf) {
   const uint4 rec = f.rec;
-  const uint32_t maxn = wave_max_u32(rec.w), maxL = wave_max_u32(rec.y);
+  const uint32_t maxn = __builtin_amdgcn_readfirstlane(wave_max_u32(rec.w));
+  const uint32_t maxL = __builtin_amdgcn_readfirstlane(wave_max_u32(rec.y));
   lb[lane] = f.lst;
   uint32_t e[16];
   const uint4* my = reinterpret_cast<const uint4*>(lb) + 4 * it_in_wave;
@@ -280,45 +309,59 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc,
                                         ((rec.x & kSlotMask) * 2 + ((rec.x >> 24) & 1)) * (HD / 2) + col, 0, 0);
   int32_t p = 0;
-  if (s == 0) {
+  auto psqt_off = [&](uint32_t x, bool live) {
+    return (live && (int)(x >> 25) == q) ? ((x & kSlotMask) * 2 + ((x >> 24) & 1)) * 4u : kDroppedOffset;
+  };
+  if constexpr (kPsqt) {
     const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
     uint32_t acc = (uint32_t)ptile[krow * kPsqtBuckets + q];
 #pragma unroll
     for (int j = 0; j < 32; ++j) acc += (uint32_t)ptile[(ent[j] >> 4) * kPsqtBuckets + q];
     p = (int32_t)acc;
+    __builtin_amdgcn_raw_buffer_store_b32(p, psqt_rsrc, psqt_off(rec.x, true), 0, 0);
   }
-  auto psqt_off = [&](uint32_t x, bool live) {
-    return (s == 0 && live && (int)(x >> 25) == q) ? ((x & kSlotMask) * 2 + ((x >> 24) & 1)) * 4u : kDroppedOffset;
-  };
-  __builtin_amdgcn_raw_buffer_store_b32(p, psqt_rsrc, psqt_off(rec.x, true), 0, 0);
   if (maxL <= 1) return;
-  // Delta positions k = 1 .. maxL-1: records at drec[c*n + root + k], fetched
-  // two ahead; a finished item (k >= L) reads past the buffer (zeros) and is
-  // masked to the zero row.
+  // Delta positions k = 1 .. maxL-1, records at drec[c*n + root + k], in
+  // batches of 8: lane q of an item loads record 8b+1+q (one 16-B load per
+  // lane per 8 positions, the next batch prefetched) and spreads the batch
+  // through the wave's LDS buffer; the 8 positions of a batch are straight-
+  // line code, so their LDS reads issue ahead of the accumulator chain.
+  // Finished items (k >= L) read the zero-filled record past the buffer and
+  // are masked to the zero row with their stores dropped.
   const uint32_t rbase = (rec.z * n + (rec.x & kSlotMask)) * 16u;
   auto fetch = [&](uint32_t k) {
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drec_rsrc, k < rec.y ? rbase + 16u * k : kDroppedOffset, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
   };
-  uint4 d1 = fetch(1), d2 = fetch(2);
+  uint4* db = dbuf + 8 * it_in_wave;
+  const uint32_t L = rec.y;
+  const uint32_t nb = __builtin_amdgcn_readfirstlane((maxL - 1 + 7) / 8);  // batches, wave-uniform
+  uint4 next = fetch(1 + q);
   u16x4 blo = lo, bhi = hi;
   int32_t pb = p;
-  for (uint32_t k = 1; k < maxL; ++k) {
-    uint4 d = d1;
-    d1 = d2;
-    d2 = fetch(k + 2);
-    const bool live = k < rec.y;
-    if (!live) d = make_uint4(0u, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
-    apply_delta(lbase, d, blo, bhi, lo, hi);
-    const uint32_t xo = live ? ((d.x & kSlotMask) * 2 + ((d.x >> 24) & 1)) * (HD / 2) + col : kDroppedOffset;
-    __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
-    int32_t pc = 0;
-    if (s == 0) pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta(ptile, d, q));
-    __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, psqt_off(d.x, live), 0, 0);
-    if constexpr (!kStar) {
-      blo = lo;
-      bhi = hi;
-      pb = pc;
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint4 batch = next;
+    next = fetch(8 * (b + 1) + 1 + q);
+    db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const uint32_t k = 8 * b + 1 + jj;
+      uint4 d = db[jj];
+      const bool live = k < L;
+      if (!live) d = make_uint4(0u, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
+      apply_delta(lbase, d, blo, bhi, lo, hi);
+      const uint32_t xo = live ? ((d.x & kSlotMask) * 2 + ((d.x >> 24) & 1)) * (HD / 2) + col : kDroppedOffset;
+      __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
+      int32_t pc = 0;
+      if constexpr (kPsqt) {
+        pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta(ptile, d, q));
+        __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, psqt_off(d.x, live), 0, 0);
+      }
+      if constexpr (!kStar) {
+        blo = lo;
+        bhi = hi;
+        pb = pc;
+      }
     }
   }
 }
@@ -338,33 +381,13 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   __shared__ uint4 img[kTileU4];
   __shared__ int32_t ptile[kTileRows * kPsqtBuckets];
   __shared__ uint2 lbuf[16][64];
-  const uint32_t w = blockIdx.x;
-  const uint32_t j = w >> 3;
-  const uint32_t unit = (j / S) * 8 + (w & 7);
-  const int s = (int)(j % S);
-  if (unit >= ctr[kNUnits]) return;
-  const int4 u = units[unit];
+  __shared__ uint4 dbuf[16][64];  // per wave: 8 positions' delta records of its 8 items
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;
   lane_item(lane, it_in_wave, q);
   constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
   constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
-  const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
-  uint4 t[kTileLoads];
-#pragma unroll
-  for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
-  uint4 pt[2];
-  const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
-  if (s == 0) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
-  }
-  u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
-  u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
-  const int krow = king_row(u.x);
-  const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
-  uint2* lb = lbuf[wv];
   // Buffer ranges are this launch's exact extents (x: n rows of HD bytes,
   // < 2^31; psqt_part: 2n words; drec: 2n records): finished items store and
   // load at kDroppedOffset, past num_records, so the hardware drops them, and
@@ -378,33 +401,64 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(flist), 0, kBufferAll, kBufferFlags);
   const __amdgpu_buffer_rsrc_t drec_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n), kBufferFlags);
-  const int last = u.z - 1;
-  int base = u.y + wv * 8;
-  SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
+  uint2* lb = lbuf[wv];
+  // Grid-stride over (unit, slice) pairs: the unit count is known only on the
+  // device and its bound (seg_max_units) is far above typical counts.  The
+  // grid is a multiple of 8 * S, so every pair keeps its XCD-aware mapping.
+  const uint32_t nunits = ctr[kNUnits];
+  for (uint32_t w = blockIdx.x;; w += gridDim.x) {
+    const uint32_t j = w >> 3;
+    const uint32_t unit = (j / S) * 8 + (w & 7);
+    const int s = (int)(j % S);
+    if (unit >= nunits) return;
+    __syncthreads();  // the previous unit's tile reads are done before the reload
+    const int4 u = units[unit];
+    const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
+    uint4 t[kTileLoads];
 #pragma unroll
-  for (int k = 0; k < kTileLoads; ++k)
-    if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
-  if (s == 0) {
-    uint4* pdst = reinterpret_cast<uint4*>(ptile);
+    for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
+    uint4 pt[2];
+    const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
+    if (s == 0) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int i = (int)threadIdx.x + 1024 * k;
-      if (i < kPtileU4) pdst[i] = i < kPtileRealU4 ? pt[k] : make_uint4(0, 0, 0, 0);
+      for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
     }
-  }
-  __syncthreads();
-  {
-    const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
-    const u32x2 klo = __builtin_shufflevector(kv, kv, 0, 1), khi = __builtin_shufflevector(kv, kv, 2, 3);
-    b_lo += __builtin_bit_cast(u16x4, klo);
-    b_hi += __builtin_bit_cast(u16x4, khi);
-  }
-  while (base < u.z) {
-    const SegFetch cur = fa;
-    fa = fetch_seg(items_rsrc, flist_rsrc, base + 128, last, lane, it_in_wave);
-    seg_pass<HD, kStar>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc,
-                        drec_rsrc);
-    base += 128;
+    u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
+    u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
+    const int krow = king_row(u.x);
+    const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
+    const int last = u.z - 1;
+    int base = u.y + wv * 8;
+    SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
+#pragma unroll
+    for (int k = 0; k < kTileLoads; ++k)
+      if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
+    if (s == 0) {
+      uint4* pdst = reinterpret_cast<uint4*>(ptile);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int i = (int)threadIdx.x + 1024 * k;
+        if (i < kPtileU4) pdst[i] = i < kPtileRealU4 ? pt[k] : make_uint4(0, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    {
+      const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
+      const u32x2 klo = __builtin_shufflevector(kv, kv, 0, 1), khi = __builtin_shufflevector(kv, kv, 2, 3);
+      b_lo += __builtin_bit_cast(u16x4, klo);
+      b_hi += __builtin_bit_cast(u16x4, khi);
+    }
+    while (base < u.z) {
+      const SegFetch cur = fa;
+      fa = fetch_seg(items_rsrc, flist_rsrc, base + 128, last, lane, it_in_wave);
+      if (s == 0)
+        seg_pass<HD, kStar, true>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
+                                  x_rsrc, drec_rsrc, dbuf[wv]);
+      else
+        seg_pass<HD, kStar, false>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
+                                   x_rsrc, drec_rsrc, dbuf[wv]);
+      base += 128;
+    }
   }
 }
 
@@ -412,7 +466,8 @@ template <int HD>
 hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& net, uint32_t n, bool star,
                          uint8_t* x, uint32_t max_units, hipStream_t stream) {
   constexpr int S = HD / 64;
-  const uint32_t groups = (max_units + 7) / 8;
+  // grid = 8 * S * G (see the kernel's grid stride); up to 8 * 64 units per sweep
+  const uint32_t groups = min((max_units + 7) / 8, 64u);
   if (star)
     hipLaunchKernelGGL((ft_segments_kernel<HD, true>), dim3(groups * 8 * S), dim3(1024), 0, stream,
                        (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, (const uint4*)G.items, P.flist,
@@ -425,6 +480,10 @@ hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& n
 }
 
 }  // namespace
+
+// units close at kSegUnitPlies positions (>= 1 item each) or kUnitItems items;
+// a unit holding fewer than kSegUnitPlies / 160 items is its king block's last
+uint32_t seg_max_units(uint32_t chunk) { return 32 + (2 * chunk + kSegUnitPlies / 160 - 1) / (kSegUnitPlies / 160); }
 
 size_t seg_scan_temp_bytes(uint32_t chunk) {
   size_t b = 0;
@@ -459,22 +518,24 @@ hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, con
   size_t tb = G.scan_temp_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(G.scan_temp, tb, G.ref, G.cref, (int)(2 * n + 1), stream)) != hipSuccess)
     return e;
-  if ((e = hipMemsetAsync(G.len, 0, 2 * (size_t)n * 4, stream)) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_items_kernel, dim3(g2), dim3(bs), 0, stream, n, bucket, G.ref, G.cref, G.ipos, G.len);
+  hipLaunchKernelGGL(seg_items_kernel, dim3(g2), dim3(bs), 0, stream, n, G.ref, G.cref, G.ipos);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_len_kernel, dim3(g2), dim3(bs), 0, stream, n, off, ngroups, base, star ? 1 : 0, bucket,
+                     G.ref, G.cref, G.ipos, G.len);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(seg_members_kernel, dim3(g2), dim3(bs), 0, stream, n, off, ngroups, base, star ? 1 : 0, bucket,
-                     G.ref, G.cref, G.ipos, (const uint4*)G.dtmp, (uint4*)G.drec, G.len);
+                     G.ref, G.cref, G.ipos, (const uint4*)G.dtmp, (uint4*)G.drec);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   uint32_t cb = (2 * n + 1023) / 1024;
   if (cb > 256) cb = 256;
   hipLaunchKernelGGL(seg_count_kernel, dim3(cb), dim3(1024), 0, stream, pos, n, G.ref, G.len, P.ctr);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(seg_scatter_kernel, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.ref, G.len,
                      P.ctr, (uint4*)G.items, P.flist);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  const uint32_t mu = sliced_max_units(n);
+  const uint32_t mu = seg_max_units(n);
 #define CALL(H) ft_segments_t<H>(G, P, net, n, star, x, mu, stream)
   FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL

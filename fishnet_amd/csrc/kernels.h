@@ -83,6 +83,7 @@ struct SegPlan {
   size_t scan_temp_bytes;
 };
 size_t seg_scan_temp_bytes(uint32_t chunk);
+uint32_t seg_max_units(uint32_t chunk);  // unit-table entries ft_segments may need
 hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
                               uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
                               uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream);

@@ -112,7 +112,24 @@ __device__ __forceinline__ int nibble_at(const uint32_t (&w)[8], int s) {
   return (int)((((i & 4) ? hi : lo) >> (4 * (s & 7))) & 15u);
 }
 
-// One workgroup of 1024 threads.
+// Segment items (ft_segments.hip) are binned by length: bin = L - 1 for
+// L <= 16, then 8 lengths per bin up to 144, then one bin for longer runs.
+__host__ __device__ constexpr uint32_t seg_len_bin(uint32_t L) {
+  return L <= 16 ? L - 1 : L <= 144 ? 16 + (L - 17) / 8 : 32;
+}
+// Segment units: contiguous item ranges of one king block holding about
+// kSegUnitPlies positions (items are sorted by length bin, a bin's items
+// counted at the bin's longest length), at most kUnitItems items.
+#ifndef SEG_UNIT_PLIES
+#define SEG_UNIT_PLIES 4096
+#endif
+constexpr uint32_t kSegUnitPlies = SEG_UNIT_PLIES;
+__host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
+  return bin < 16 ? bin + 1 : bin < 32 ? 8 * bin - 104 : 160;
+}
+
+// One workgroup of 1024 threads.  unit_items = 0: segment units (see
+// kSegUnitPlies) instead of fixed-size ones.
 __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ ctr, int4* __restrict__ units,
                                                          uint32_t unit_items) {
   __shared__ uint32_t s[kBins];
@@ -153,7 +170,48 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
     ctr[kOff + i] = s[i];
     ctr[kCur + i] = s[i];
   }
-  if (t < 32) {
+  if (unit_items == 0) {
+    if (t < 32) {
+      // One lane per king block walks its 33 length bins twice: count the
+      // units, then (after a wave prefix sum) write them.
+      const int kb = t;
+      auto walk = [&](bool emit, uint32_t nu) -> uint32_t {
+        uint32_t start = s[kb * 33], items = 0, plies = 0;
+        for (int b = 0; b < 33; ++b) {
+          const int i = kb * 33 + b;  // bin sizes from the LDS offsets (the last bin from the total)
+          const uint32_t cnt = (i + 1 < kItemBins ? s[i + 1] : s[kItemBins - 1] + ctr[kCnt + kItemBins - 1]) - s[i];
+          const uint32_t w = seg_bin_longest(b);
+          for (uint32_t left = cnt; left > 0;) {
+            uint32_t take = (kSegUnitPlies - plies + w - 1) / w;
+            take = min(min(take, left), kUnitItems - items);
+            items += take;
+            plies += take * w;
+            left -= take;
+            if (plies >= kSegUnitPlies || items >= kUnitItems) {
+              if (emit) units[nu] = make_int4(kb, (int)start, (int)(start + items), 0);
+              ++nu;
+              start += items;
+              items = plies = 0;
+            }
+          }
+        }
+        if (items) {
+          if (emit) units[nu] = make_int4(kb, (int)start, (int)(start + items), 0);
+          ++nu;
+        }
+        return nu;
+      };
+      const uint32_t mine = walk(false, 0);
+      uint32_t incl = mine;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, 32);
+        if (kb >= o) incl += v;
+      }
+      walk(true, incl - mine);
+      if (kb == 31) ctr[kNUnits] = incl;
+    }
+  } else if (t < 32) {
     // Unit table: each king block's item range in chunks of <= unit_items;
     // lane kb counts its block's units, a wave prefix sum places them.
     const int kb = t;
