@@ -179,17 +179,20 @@ __device__ __forceinline__ uint32_t seg_key(const LaneBoard& b, int c, uint32_t 
   return (uint32_t)king_block(c, c ? b.bk : b.wk) * 33u + seg_len_bin(L);
 }
 
+// Both sort kernels run one thread per item k < cref[2n] (refresh of
+// perspective k >= cref[n]); invalid positions are refreshes with len 0.
 __global__ __launch_bounds__(1024) void seg_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                                         const uint32_t* __restrict__ ref,
+                                                         const uint32_t* __restrict__ cref,
+                                                         const uint32_t* __restrict__ ipos,
                                                          const uint32_t* __restrict__ len,
                                                          uint32_t* __restrict__ ctr) {
   __shared__ uint32_t h[kItemBins];
   for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) h[i] = 0;
   __syncthreads();
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < 2 * n; j += gridDim.x * blockDim.x) {
-    if (!ref[j] || !len[j]) continue;  // len = 0: invalid position
-    const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
-    atomicAdd(&h[seg_key(lane_decode(pos + i), (int)c, len[j])], 1u);
+  const uint32_t K = cref[2 * n], K0 = cref[n];
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
+    const uint32_t c = k >= K0 ? 1u : 0u, i = ipos[k], L = len[c * n + i];
+    if (L) atomicAdd(&h[seg_key(lane_decode(pos + i), (int)c, L)], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kItemBins; i += blockDim.x)
@@ -199,28 +202,31 @@ __global__ __launch_bounds__(1024) void seg_count_kernel(const fnnue_pos* __rest
 // Sorted item record: {root | half << 24 | bucket << 25, length, perspective,
 // piece count}; full feature list of the root as in the sliced plan.
 __global__ __launch_bounds__(1024) void seg_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                                           const uint32_t* __restrict__ ref,
+                                                           const uint32_t* __restrict__ cref,
+                                                           const uint32_t* __restrict__ ipos,
                                                            const uint32_t* __restrict__ len,
                                                            uint32_t* __restrict__ ctr, uint4* __restrict__ items,
                                                            uint16_t* __restrict__ flist) {
   __shared__ uint32_t lcnt[kItemBins];
   __shared__ uint32_t lbase[kItemBins];
+  const uint32_t K = cref[2 * n], K0 = cref[n];
+  if (blockIdx.x * blockDim.x >= K) return;  // workgroup-uniform
   for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = j < 2 * n && ref[j] && len[j];
-  const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t c = k >= K0 ? 1u : 0u, i = k < K ? ipos[k] : 0u;
+  const uint32_t L = k < K ? len[c * n + i] : 0u;
+  const bool live = L != 0;
   LaneBoard b;
-  uint32_t key = 0, rk = 0, L = 0;
+  uint32_t key = 0, rk = 0;
   if (live) {
     b = lane_decode(pos + i);
-    L = len[j];
     key = seg_key(b, (int)c, L);
     rk = atomicAdd(&lcnt[key], 1u);
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < kItemBins; k += blockDim.x)
-    lbase[k] = lcnt[k] ? atomicAdd(&ctr[kCur + k], lcnt[k]) : 0;
+  for (int t = threadIdx.x; t < kItemBins; t += blockDim.x)
+    lbase[t] = lcnt[t] ? atomicAdd(&ctr[kCur + t], lcnt[t]) : 0;
   __syncthreads();
   if (!live) return;
   const uint32_t slot = lbase[key] + rk;
@@ -528,12 +534,12 @@ hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, con
   if ((e = hipGetLastError()) != hipSuccess) return e;
   uint32_t cb = (2 * n + 1023) / 1024;
   if (cb > 256) cb = 256;
-  hipLaunchKernelGGL(seg_count_kernel, dim3(cb), dim3(1024), 0, stream, pos, n, G.ref, G.len, P.ctr);
+  hipLaunchKernelGGL(seg_count_kernel, dim3(cb), dim3(1024), 0, stream, pos, n, G.cref, G.ipos, G.len, P.ctr);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_scatter_kernel, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.ref, G.len,
-                     P.ctr, (uint4*)G.items, P.flist);
+  hipLaunchKernelGGL(seg_scatter_kernel, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.cref, G.ipos,
+                     G.len, P.ctr, (uint4*)G.items, P.flist);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint32_t mu = seg_max_units(n);
 #define CALL(H) ft_segments_t<H>(G, P, net, n, star, x, mu, stream)

@@ -171,45 +171,54 @@ __global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ 
     ctr[kCur + i] = s[i];
   }
   if (unit_items == 0) {
+    // Segment units: unit u of king block kb starts at the first item whose
+    // cumulative positions (a bin's items counted at the bin's longest run)
+    // reach u * kSegUnitPlies.  Bins are contiguous in item order, so each
+    // (kb, bin) thread places the unit starts falling inside its bin.
+    __shared__ uint32_t pb[kItemBins];  // positions before bin i within its king block
+    __shared__ uint32_t ubase[33];      // first unit of each king block
+    for (int k = 0; k < per; ++k) {     // local[k] = count of bin t*per + k
+      const int i = t * per + k;
+      if (i < kItemBins) pb[i] = local[k] * seg_bin_longest(i % 33);
+    }
+    __syncthreads();
     if (t < 32) {
-      // One lane per king block walks its 33 length bins twice: count the
-      // units, then (after a wave prefix sum) write them.
-      const int kb = t;
-      auto walk = [&](bool emit, uint32_t nu) -> uint32_t {
-        uint32_t start = s[kb * 33], items = 0, plies = 0;
-        for (int b = 0; b < 33; ++b) {
-          const int i = kb * 33 + b;  // bin sizes from the LDS offsets (the last bin from the total)
-          const uint32_t cnt = (i + 1 < kItemBins ? s[i + 1] : s[kItemBins - 1] + ctr[kCnt + kItemBins - 1]) - s[i];
-          const uint32_t w = seg_bin_longest(b);
-          for (uint32_t left = cnt; left > 0;) {
-            uint32_t take = (kSegUnitPlies - plies + w - 1) / w;
-            take = min(min(take, left), kUnitItems - items);
-            items += take;
-            plies += take * w;
-            left -= take;
-            if (plies >= kSegUnitPlies || items >= kUnitItems) {
-              if (emit) units[nu] = make_int4(kb, (int)start, (int)(start + items), 0);
-              ++nu;
-              start += items;
-              items = plies = 0;
-            }
-          }
-        }
-        if (items) {
-          if (emit) units[nu] = make_int4(kb, (int)start, (int)(start + items), 0);
-          ++nu;
-        }
-        return nu;
-      };
-      const uint32_t mine = walk(false, 0);
+      uint32_t run = 0;
+      for (int b = 0; b < 33; ++b) {
+        const uint32_t v = pb[t * 33 + b];
+        pb[t * 33 + b] = run;
+        run += v;
+      }
+      const uint32_t mine = (run + kSegUnitPlies - 1) / kSegUnitPlies;
       uint32_t incl = mine;
 #pragma unroll
       for (int o = 1; o < 32; o <<= 1) {
         const uint32_t v = __shfl_up(incl, o, 32);
-        if (kb >= o) incl += v;
+        if (t >= o) incl += v;
       }
-      walk(true, incl - mine);
-      if (kb == 31) ctr[kNUnits] = incl;
+      ubase[t] = incl - mine;
+      if (t == 31) {
+        ubase[32] = incl;
+        ctr[kNUnits] = incl;
+      }
+    }
+    __syncthreads();
+    for (int k = 0; k < per; ++k) {
+      const int i = t * per + k;
+      if (i >= kItemBins || local[k] == 0) continue;
+      const int kb = i / 33;
+      const uint32_t w = seg_bin_longest(i % 33), p0 = pb[i], p1 = p0 + local[k] * w;
+      for (uint32_t u = (p0 + kSegUnitPlies - 1) / kSegUnitPlies; u * kSegUnitPlies < p1; ++u)
+        units[ubase[kb] + u] = make_int4(kb, (int)(s[i] + (u * kSegUnitPlies - p0 + w - 1) / w), 0, 0);
+    }
+    __syncthreads();  // the starts are visible to the whole workgroup
+    // Ends: the next unit's start, or the block's end.  Only .z is written
+    // here, so reading a neighbour's .y does not race.  (Unit 0 of a block
+    // starts at its first non-empty bin's offset, i.e. the block's first item.)
+    for (uint32_t v = t; v < ubase[32]; v += 1024) {
+      const int kb = units[v].x;
+      const uint32_t kb_end = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
+      units[v].z = v + 1 < ubase[kb + 1] ? units[v + 1].y : (int)kb_end;
     }
   } else if (t < 32) {
     // Unit table: each king block's item range in chunks of <= unit_items;
