@@ -43,9 +43,13 @@ int hip_fail(hipError_t e, const char* what) {
     if (_e != hipSuccess) return hip_fail(_e, what); \
   } while (0)
 
-// Positions per launch pair; the transformed-feature workspace is
-// kChunk * hd bytes (1 GiB at hd = 1024).
+// Positions per launch pair: 2^20, fewer for hd > 2047 so the transformed-
+// feature workspace (chunk * hd bytes, 1 GiB at hd = 1024) stays inside one
+// raw buffer resource (num_records <= 2^31 - 1).
 constexpr uint32_t kChunk = 1u << 20;
+uint32_t chunk_for_hd(uint32_t hd) {
+  return std::min<uint32_t>(kChunk, (0x7FFFFFFFu / hd) & ~1023u);
+}
 
 }  // namespace
 
@@ -59,8 +63,9 @@ struct fnnue_ctx {
   uint8_t* image = nullptr;
   size_t image_bytes = 0;
   NetPtrs ptrs{};
-  uint8_t* x = nullptr;        // [kChunk][hd] transformed features
-  uint8_t* bucket = nullptr;   // [kChunk]
+  uint32_t chunk = 0;          // positions per launch pair (chunk_for_hd)
+  uint8_t* x = nullptr;        // [chunk][hd] transformed features
+  uint8_t* bucket = nullptr;   // [chunk]
   uint32_t* err = nullptr;     // latched position errors
   hipStream_t stream = nullptr;
   // host-API staging
@@ -133,21 +138,23 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
   if (!c) return fail(FNNUE_E_OOM, "host allocation failed");
   c->device = device;
   c->hd = hd;
+  c->chunk = chunk_for_hd(hd);
+  const uint32_t chunk = c->chunk;
   DeviceGuard g(device);
   c->image_bytes = image_layout(hd).total;
   if (hipMalloc(&c->image, c->image_bytes) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (net image)");
-  if (hipMalloc(&c->x, (size_t)kChunk * hd) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
-  if (hipMalloc(&c->bucket, kChunk) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
+  if (hipMalloc(&c->x, (size_t)chunk * hd) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
+  if (hipMalloc(&c->bucket, chunk) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
   if (hipMalloc(&c->err, sizeof(uint32_t)) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (error word)");
   HIP_TRY(hipMemset(c->err, 0, sizeof(uint32_t)), "hipMemset");
   SlicedPlan& P = c->plan;
   if (hipMalloc(&P.tiles, sliced_tiles_bytes(hd)) != hipSuccess ||
       hipMalloc(&P.ctr, sliced_ctr_words() * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&P.units, (size_t)std::max(sliced_max_units(kChunk), seg_max_units(kChunk)) * 16) != hipSuccess ||
-      hipMalloc(&P.items, (size_t)2 * kChunk * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&P.flist, (size_t)2 * kChunk * 32 * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&P.perm, (size_t)kChunk * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&P.psqt_part, (size_t)2 * kChunk * sizeof(int32_t)) != hipSuccess)
+      hipMalloc(&P.units, (size_t)std::max(sliced_max_units(chunk), seg_max_units(chunk)) * 16) != hipSuccess ||
+      hipMalloc(&P.items, (size_t)2 * chunk * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.flist, (size_t)2 * chunk * 32 * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&P.perm, (size_t)chunk * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.psqt_part, (size_t)2 * chunk * sizeof(int32_t)) != hipSuccess)
     return fail(FNNUE_E_OOM, "device allocation (sliced plan)");
   if (const char* impl = std::getenv("FNNUE_FT_IMPL"))
     c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
@@ -232,8 +239,8 @@ int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
 int ensure_seg(fnnue_ctx* c) {
   SegPlan& G = c->seg;
   if (G.ref) return FNNUE_OK;
-  const size_t n2 = 2 * (size_t)kChunk;
-  G.scan_temp_bytes = seg_scan_temp_bytes(kChunk);
+  const size_t n2 = 2 * (size_t)c->chunk;
+  G.scan_temp_bytes = seg_scan_temp_bytes(c->chunk);
   if (hipMalloc(&G.ref, (n2 + 1) * 4) != hipSuccess || hipMalloc(&G.cref, (n2 + 1) * 4) != hipSuccess ||
       hipMalloc(&G.dtmp, n2 * 16) != hipSuccess || hipMalloc(&G.drec, n2 * 16) != hipSuccess ||
       hipMalloc(&G.ipos, n2 * 4) != hipSuccess || hipMalloc(&G.len, n2 * 4) != hipSuccess ||
@@ -435,8 +442,8 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
   if (!d_pos || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  for (size_t b = 0; b < n; b += kChunk) {
-    const uint32_t m = (uint32_t)std::min<size_t>(kChunk, n - b);
+  for (size_t b = 0; b < n; b += ctx->chunk) {
+    const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
     std::array<hipEvent_t, 3>* ev = nullptr;
     int rc = next_events(ctx, &ev);
     if (rc) return rc;
@@ -480,7 +487,7 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
   size_t gb = 0;
   while (gb < ngroups) {
     size_t ge = gb;
-    while (ge < ngroups && off[ge + 1] - off[gb] <= kChunk) {
+    while (ge < ngroups && off[ge + 1] - off[gb] <= ctx->chunk) {
       if (off[ge + 1] < off[ge]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
       ++ge;
     }
@@ -521,7 +528,7 @@ int fnnue_eval_positions(fnnue_ctx* ctx, const fnnue_pos* pos, size_t n, int32_t
   for (size_t i = 0; i < n; ++i)
     if (!valid_host_pos(pos[i])) return fail(FNNUE_E_POSITION, "invalid position at index " + std::to_string(i));
   DeviceGuard g(ctx->device);
-  const size_t step = std::min<size_t>(n, 4 * (size_t)kChunk);
+  const size_t step = std::min<size_t>(n, 4 * (size_t)ctx->chunk);
   int rc = ensure_stage(ctx, step, 0);
   if (rc) return rc;
   for (size_t b = 0; b < n; b += step) {

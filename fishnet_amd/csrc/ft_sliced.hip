@@ -308,7 +308,10 @@ uint32_t sliced_max_units(uint32_t chunk) { return 32 + (2 * chunk + kUnitItems 
     case 256: return CALL(256);     \
     case 512: return CALL(512);     \
     case 1024: return CALL(1024);   \
+    case 1536: return CALL(1536);   \
     case 2048: return CALL(2048);   \
+    case 2560: return CALL(2560);   \
+    case 3072: return CALL(3072);   \
     default: return hipErrorInvalidValue; \
   }
 

@@ -4,8 +4,9 @@
 //   ft_scratch  HalfKAv2_hm feature indices + FeatureTransformer refresh +
 //               transform (clamp, pairwise product) + PSQT term.  One 64-lane
 //               wave per position; the wave owns both int16 accumulators in
-//               VGPRs: lane l holds elements [l*EPL, l*EPL+EPL) of each half,
-//               so every weight-row read is a 1 KiB-contiguous wave load
+//               VGPRs: lane l holds elements [l*EPL, l*EPL+EPL) of each half
+//               (HD/128 not a power of two: pieces, see Lanes), so every
+//               weight-row read is a 1 KiB-contiguous wave load
 //               (HD=1024: global_load_dwordx4 per lane) and the pairwise
 //               product (j, j+HD/2) never crosses lanes.
 //   ft_groups   Same, but walking a group of positions (a game's plies, or a
@@ -40,16 +41,53 @@ __device__ __forceinline__ void transform_store(typename Vec<EPL>::u16 lo, typen
   *reinterpret_cast<typename Vec<EPL>::u8*>(dst) = __builtin_convertvector(prod, typename Vec<EPL>::u8);
 }
 
+// One wave's share of an accumulator half (HD/2 int16): lane l holds K
+// pieces of P = lowest power of two dividing HD/128 columns, piece k at
+// columns 64Pk + Pl .. +P-1.  Vector types only come in power-of-two sizes
+// (an ext_vector of 12 elements occupies 16), so HD = 1536/2560/3072 use K =
+// 3/5/3 pieces; every piece is one fully coalesced wave access.
+template <int HD>
+struct Lanes {
+  static constexpr int kEpl = HD / 128, kP = kEpl & -kEpl, kK = kEpl / kP;
+  typedef typename Vec<kP>::u16 u16;
+  u16 v[kK];
+  __device__ __forceinline__ static Lanes load(const int16_t* half, int lane) {
+    Lanes r;
+    const u16* p = reinterpret_cast<const u16*>(half);
+#pragma unroll
+    for (int k = 0; k < kK; ++k) r.v[k] = p[64 * k + lane];
+    return r;
+  }
+  __device__ __forceinline__ Lanes& operator+=(const Lanes& o) {
+#pragma unroll
+    for (int k = 0; k < kK; ++k) v[k] += o.v[k];
+    return *this;
+  }
+  __device__ __forceinline__ Lanes& operator-=(const Lanes& o) {
+#pragma unroll
+    for (int k = 0; k < kK; ++k) v[k] -= o.v[k];
+    return *this;
+  }
+  // transformed output of one perspective: dst = that perspective's HD/2 bytes
+  __device__ __forceinline__ static void transform(const Lanes& lo, const Lanes& hi, uint8_t* dst, int lane) {
+#pragma unroll
+    for (int k = 0; k < kK; ++k) transform_store<kP>(lo.v[k], hi.v[k], dst + kP * (64 * k + lane));
+  }
+  __device__ __forceinline__ static void zero(uint8_t* dst, int lane) {
+#pragma unroll
+    for (int k = 0; k < kK; ++k)
+      *reinterpret_cast<typename Vec<kP>::u8*>(dst + kP * (64 * k + lane)) = (typename Vec<kP>::u8)0;
+  }
+};
+
 // Adds (SIGN=+1) or subtracts the weight rows f(s) for every square s in `mask`
 // to the lane's accumulator slice.  f is a per-lane value read with readlane,
 // so each row address is wave-uniform (scalar base + lane offset) and each row
 // is two 1 KiB-contiguous wave loads (HD=1024).  U rows are in flight per step.
 template <int HD, int U>
 __device__ __forceinline__ void add_rows(const int16_t* __restrict__ ftw, uint64_t mask, int f_add, int f_sub,
-                                         bool do_sub, typename Vec<HD / 128>::u16& lo,
-                                         typename Vec<HD / 128>::u16& hi, int lane) {
-  constexpr int EPL = HD / 128;
-  typedef typename Vec<EPL>::u16 u16;
+                                         bool do_sub, Lanes<HD>& lo, Lanes<HD>& hi, int lane) {
+  typedef Lanes<HD> L;
   while (mask) {
     int fa[U], fs[U];
 #pragma unroll
@@ -64,16 +102,16 @@ __device__ __forceinline__ void add_rows(const int16_t* __restrict__ ftw, uint64
         fs[u] = kZeroRow;
       }
     }
-    u16 va[U][2], vs[U][2];
+    L va[U][2], vs[U][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const u16* ra = reinterpret_cast<const u16*>(ftw + (size_t)fa[u] * HD);
-      va[u][0] = ra[lane];
-      va[u][1] = ra[64 + lane];
+      const int16_t* ra = ftw + (size_t)fa[u] * HD;
+      va[u][0] = L::load(ra, lane);
+      va[u][1] = L::load(ra + HD / 2, lane);
       if (do_sub) {
-        const u16* rs = reinterpret_cast<const u16*>(ftw + (size_t)fs[u] * HD);
-        vs[u][0] = rs[lane];
-        vs[u][1] = rs[64 + lane];
+        const int16_t* rs = ftw + (size_t)fs[u] * HD;
+        vs[u][0] = L::load(rs, lane);
+        vs[u][1] = L::load(rs + HD / 2, lane);
       }
     }
 #pragma unroll
@@ -103,10 +141,8 @@ __device__ __forceinline__ int psqt_term(const int32_t* __restrict__ psqw, const
 
 template <int HD>
 __device__ __forceinline__ void store_invalid(uint8_t* x, int lane) {
-  constexpr int EPL = HD / 128;
-  const typename Vec<EPL>::u8 z = (typename Vec<EPL>::u8)0;
-  *reinterpret_cast<typename Vec<EPL>::u8*>(x + lane * EPL) = z;
-  *reinterpret_cast<typename Vec<EPL>::u8*>(x + HD / 2 + lane * EPL) = z;
+  Lanes<HD>::zero(x, lane);
+  Lanes<HD>::zero(x + HD / 2, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -115,13 +151,11 @@ template <int HD, int U>
 __global__ __launch_bounds__(256) void ft_scratch_kernel(const fnnue_pos* __restrict__ pos, uint32_t n, NetPtrs net,
                                                          uint8_t* __restrict__ x, int32_t* __restrict__ psqt,
                                                          uint8_t* __restrict__ bucket_out, uint32_t* __restrict__ err) {
-  constexpr int EPL = HD / 128;
-  typedef typename Vec<EPL>::u16 u16;
+  typedef Lanes<HD> u16;
   const int lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  const u16* bias = reinterpret_cast<const u16*>(net.ft_bias);
-  const u16 b_lo = bias[lane], b_hi = bias[64 + lane];
+  const u16 b_lo = u16::load(net.ft_bias, lane), b_hi = u16::load(net.ft_bias + HD / 2, lane);
   for (uint32_t p = wid; p < n; p += nw) {
     const Decoded d = decode(pos + p, lane);
     uint8_t* xo = x + (size_t)p * HD;
@@ -164,12 +198,12 @@ __global__ __launch_bounds__(256) void ft_scratch_kernel(const fnnue_pos* __rest
       u16 r0[U][2], r1[U][2];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const u16* a = reinterpret_cast<const u16*>(net.ft_w + (size_t)f0[u] * HD);
-        const u16* b = reinterpret_cast<const u16*>(net.ft_w + (size_t)f1[u] * HD);
-        r0[u][0] = a[lane];
-        r0[u][1] = a[64 + lane];
-        r1[u][0] = b[lane];
-        r1[u][1] = b[64 + lane];
+        const int16_t* a = net.ft_w + (size_t)f0[u] * HD;
+        const int16_t* b = net.ft_w + (size_t)f1[u] * HD;
+        r0[u][0] = u16::load(a, lane);
+        r0[u][1] = u16::load(a + HD / 2, lane);
+        r1[u][0] = u16::load(b, lane);
+        r1[u][1] = u16::load(b + HD / 2, lane);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -180,11 +214,11 @@ __global__ __launch_bounds__(256) void ft_scratch_kernel(const fnnue_pos* __rest
       }
     }
     if (d.stm) {
-      transform_store<EPL>(k_lo, k_hi, xo + lane * EPL);
-      transform_store<EPL>(w_lo, w_hi, xo + HD / 2 + lane * EPL);
+      u16::transform(k_lo, k_hi, xo, lane);
+      u16::transform(w_lo, w_hi, xo + HD / 2, lane);
     } else {
-      transform_store<EPL>(w_lo, w_hi, xo + lane * EPL);
-      transform_store<EPL>(k_lo, k_hi, xo + HD / 2 + lane * EPL);
+      u16::transform(w_lo, w_hi, xo, lane);
+      u16::transform(k_lo, k_hi, xo + HD / 2, lane);
     }
     if (lane == 0) {
       psqt[p] = tot / 2;
@@ -205,13 +239,11 @@ __global__ __launch_bounds__(256) void ft_groups_kernel(const fnnue_pos* __restr
                                                         uint8_t* __restrict__ x, int32_t* __restrict__ psqt,
                                                         uint8_t* __restrict__ bucket_out,
                                                         uint32_t* __restrict__ err) {
-  constexpr int EPL = HD / 128;
-  typedef typename Vec<EPL>::u16 u16;
+  typedef Lanes<HD> u16;
   const int lane = threadIdx.x & 63;
   const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  const u16* bias = reinterpret_cast<const u16*>(net.ft_bias);
-  const u16 b_lo = bias[lane], b_hi = bias[64 + lane];
+  const u16 b_lo = u16::load(net.ft_bias, lane), b_hi = u16::load(net.ft_bias + HD / 2, lane);
   for (uint32_t g = wid; g < ngroups; g += nw) {
     const uint32_t begin = off[g], end = off[g + 1];
     // Base state (previous ply for CHAIN, parent for STAR).
@@ -266,11 +298,11 @@ __global__ __launch_bounds__(256) void ft_groups_kernel(const fnnue_pos* __restr
         }
       }
       if (d.stm) {
-        transform_store<EPL>(k_lo, k_hi, xo + lane * EPL);
-        transform_store<EPL>(w_lo, w_hi, xo + HD / 2 + lane * EPL);
+        u16::transform(k_lo, k_hi, xo, lane);
+        u16::transform(w_lo, w_hi, xo + HD / 2, lane);
       } else {
-        transform_store<EPL>(w_lo, w_hi, xo + lane * EPL);
-        transform_store<EPL>(k_lo, k_hi, xo + HD / 2 + lane * EPL);
+        u16::transform(w_lo, w_hi, xo, lane);
+        u16::transform(k_lo, k_hi, xo + HD / 2, lane);
       }
       if (lane == 0) {
         psqt[o] = tot;
@@ -517,7 +549,8 @@ hipError_t launch_stack_t(const uint8_t* x, const uint8_t* bucket, uint32_t n, c
 }  // namespace
 
 bool kernels_support_hd(uint32_t hd) {
-  return hd == 128 || hd == 256 || hd == 512 || hd == 1024 || hd == 2048;
+  return hd == 128 || hd == 256 || hd == 512 || hd == 1024 || hd == 1536 || hd == 2048 || hd == 2560 ||
+         hd == 3072;
 }
 
 #define FNNUE_HD_DISPATCH(hd, CALL) \
@@ -526,7 +559,10 @@ bool kernels_support_hd(uint32_t hd) {
     case 256: return CALL(256);     \
     case 512: return CALL(512);     \
     case 1024: return CALL(1024);   \
+    case 1536: return CALL(1536);   \
     case 2048: return CALL(2048);   \
+    case 2560: return CALL(2560);   \
+    case 3072: return CALL(3072);   \
     default: return hipErrorInvalidValue; \
   }
 

@@ -61,8 +61,10 @@ class Net:
         return buf
 
     def __del__(self):
-        if getattr(self, "_h", None) and self._h.value:
-            N.lib.fnnue_net_free(self._h)
+        # at interpreter shutdown the module globals may already be gone
+        lib = getattr(N, "lib", None) if N is not None else None
+        if lib is not None and getattr(self, "_h", None) and self._h.value:
+            lib.fnnue_net_free(self._h)
             self._h = C.c_void_p()
 
 
@@ -174,7 +176,8 @@ class Evaluator:
             self._h = C.c_void_p()
 
     def __del__(self):
-        self.close()
+        if N is not None and getattr(N, "lib", None) is not None:
+            self.close()
 
 
 def pos_from_fen(fen: str) -> np.ndarray:

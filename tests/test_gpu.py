@@ -57,8 +57,12 @@ def test_random_playouts_big_net(ev_cache):
     assert_same(ev, on, F.random_playouts(1, 20000, threads=8))
 
 
+# later-SF widths: 1536, 2560, 3072 run the same kernels
+WIDE = [(8, 1536, N.SYNTH_LEB128), (9, 2560, 0), (10, 3072, N.SYNTH_WRAP)]
+
+
 @pytest.mark.parametrize("seed,hd,flags", [(7, 128, 0), (4, 256, N.SYNTH_FC1_PAD), (2, 512, N.SYNTH_LEB128),
-                                           (3, 1024, N.SYNTH_WRAP), (6, 2048, 0)])
+                                           (3, 1024, N.SYNTH_WRAP), (6, 2048, 0)] + WIDE)
 def test_other_nets(ev_cache, seed, hd, flags):
     ev, on = ev_cache(seed, hd, flags)
     assert_same(ev, on, F.random_playouts(seed + 100, 3000, threads=8))
@@ -75,7 +79,8 @@ def test_ragged_batch_sizes(ev_cache, n, impl):
         ev.set_ft_impl(N.FT_SLICED)
 
 
-@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (3, 1024, N.SYNTH_WRAP), (6, 2048, 0)])
+@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (3, 1024, N.SYNTH_WRAP), (6, 2048, 0),
+                                           WIDE[2]])
 def test_ft_impls_agree(ev_cache, seed, hd, flags):
     """LDS-stationary (sliced) and per-position gather feature transformers."""
     ev, on = ev_cache(seed, hd, flags)
@@ -88,6 +93,26 @@ def test_ft_impls_agree(ev_cache, seed, hd, flags):
     idx = np.arange(0, len(pos), 7)
     ops, opo, rc = on.eval_packed(pos[idx], threads=8)
     assert np.array_equal(a[0][idx], ops) and np.array_equal(a[1][idx], opo)
+
+
+def test_chunk_boundary_wide_net(ev_cache):
+    """HD = 3072 runs in chunks of 698368 positions (chunk * hd < 2^31, one
+    buffer resource): a batch crossing the boundary, positions and CHAIN
+    groups, is exact on both sides of it."""
+    ev, on = ev_cache(*WIDE[2])
+    chunk = min(1 << 20, (0x7FFFFFFF // 3072) & ~1023)
+    pos = F.random_playouts(31, chunk + 3000, threads=8)
+    ps, po = ev.eval_positions(pos)
+    idx = np.r_[0:2000, chunk - 2000:chunk + 3000]
+    ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+    assert np.array_equal(ps[idx], ops) and np.array_equal(po[idx], opo)
+    gpos, off = F.random_playouts(32, 9000, mode=N.PLAYOUT_PLIES, threads=8)
+    assert off[-1] > chunk
+    gs, go = ev.eval_groups(gpos, off, N.GROUP_CHAIN)
+    cut = int(np.searchsorted(off, chunk, side="right")) - 1  # first group of the second chunk
+    idx = np.r_[0:2000, int(off[cut]) - 2000:int(off[cut]) + 2000, len(gpos) - 2000:len(gpos)]
+    ops, opo, rc = on.eval_packed(gpos[idx], threads=8)
+    assert np.array_equal(gs[idx], ops) and np.array_equal(go[idx], opo)
 
 
 def test_same_king_block_everywhere(ev_cache):
@@ -206,7 +231,7 @@ def test_image_broadcast_path(ev_cache):
     ev2.close()
 
 
-@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (6, 2048, 0), (3, 1024, N.SYNTH_WRAP)])
+@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (6, 2048, 0), (3, 1024, N.SYNTH_WRAP)] + WIDE)
 def test_group_impls_agree(ev_cache, seed, hd, flags):
     """Incremental groups: LDS-tile segments (sliced, default) == per-group
     gather kernel == oracle, for CHAIN games and STAR children."""

@@ -48,7 +48,8 @@ def _sample_positions(n=40, seed=5):
 
 
 @pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (3, 1024, N.SYNTH_WRAP),
-                                           (4, 256, N.SYNTH_FC1_PAD)])
+                                           (4, 256, N.SYNTH_FC1_PAD), (8, 1536, 0),
+                                           (10, 3072, N.SYNTH_WRAP)])
 def test_oracle_matches_numpy_restatement(seed, hd, flags):
     data = net_bytes(seed, hd, flags)
     on = O.OracleNet(data)
