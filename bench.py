@@ -200,7 +200,16 @@ def main():
     positional = d_positional.cpu().numpy()
     cpu = None
     parity = None
-    if rank == 0 and not args.no_cpu_baseline:
+    gathered = None
+    if dist_on:
+        # Evals gathered back to rank 0 over RCCL (north star: "evals are gathered
+        # back"), outside the timed region: 8 B per position.
+        g_ps = D.gather_to_rank0(psqt, dev)
+        g_po = D.gather_to_rank0(positional, dev)
+        if rank == 0:
+            gathered = {"positions": int(g_ps.size), "equals_sum_of_shards": bool(g_ps.size == g_po.size
+                                                                                  == int(total_positions))}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle.oracle import OracleNet  # cpu_baseline leg: the oracle is the timed CPU port
         on = OracleNet(F.synthesize_net(args.seed, args.hd, 0))
         done, mism, t0 = 0, 0, time.perf_counter()
@@ -270,14 +279,18 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "issue": issue,
-                "kernel": ("ft_slices_kernel + plan_* (LDS-stationary FT)" if off is None and args.ft_impl == "sliced"
-                           else "ft_scratch_kernel" if off is None else "ft_groups_kernel"),
+                "kernel": {("positions", "sliced"): "ft_slices_kernel + plan_* (LDS-stationary FT)",
+                           ("positions", "gather"): "ft_scratch_kernel",
+                           ("groups", "sliced"): "ft_segments_kernel + seg_* plan (incremental on LDS tiles)",
+                           ("groups", "gather"): "ft_groups_kernel"}[("positions" if off is None else "groups",
+                                                                     args.ft_impl)],
                 "kernel_avg_ms": round(ft_avg_ms, 4),
                 "stack_kernel_avg_ms": round(stack_avg_ms, 4),
                 "algorithmic_bytes_per_launch": int(bytes_per_launch),
             },
             "cpu_baseline": cpu,
             "parity_spot_check": parity,
+            "gathered": gathered,
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
         print(json.dumps(out), flush=True)

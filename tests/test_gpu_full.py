@@ -1,0 +1,106 @@
+"""Full-size parity run (north star: "bit-exact NNUE evals for >= 1e8 positions
+per run"): BASELINE config 4's workload — every ply of random games plus all
+their legal 1-ply children, >= 1e8 positions — evaluated on one MI355X by both
+device paths (incremental STAR groups and from-scratch sliced), and EVERY
+result compared with the CPU oracle.
+
+Opt-in (it takes about a minute of host time): FNNUE_FULL=<positions> on the
+GPU box, e.g.
+    FNNUE_FULL=100000000 python -u -m pytest tests/test_gpu_full.py -m gpu -s
+A JSON record goes to gpurun_out/full_parity.json.
+"""
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+
+import fishnet_amd as F
+from oracle.oracle import OracleNet
+from tests.conftest import ROOT, net_bytes
+
+pytestmark = pytest.mark.gpu
+
+TARGET = int(os.environ.get("FNNUE_FULL", "0"))
+
+
+@pytest.mark.skipif(TARGET <= 0, reason="opt-in: set FNNUE_FULL=<positions>")
+def test_full_size_parity():
+    import torch
+
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    pos_parts, off_parts, total, seed, base = [], [np.zeros(1, np.int64)], 0, 3, 0
+    while total < TARGET:  # config 4: seed 3, games of U[0,160] plies + all legal children
+        p, o = F.random_playouts(seed, 4000, 0, 160, mode=F.PLAYOUT_CHILDREN, threads=threads)
+        pos_parts.append(p)
+        off_parts.append(o[1:].astype(np.int64) + base)
+        base += len(p)
+        total += len(p)
+        seed += 7919
+    pos = np.concatenate(pos_parts)
+    off = np.concatenate(off_parts)
+    del pos_parts
+    t_gen = time.time() - t0
+    n, ng = len(pos), len(off) - 1
+    print(f"generated {n} positions in {ng} STAR groups in {t_gen:.1f} s", flush=True)
+    assert n >= TARGET and n < 2 ** 31
+
+    data = net_bytes(1, 1024, 0)
+    ev = F.Evaluator(F.Net.from_bytes(data), 0)
+    dev = torch.device("cuda", 0)
+    d_pos = torch.from_numpy(pos).to(dev)
+    d_off = torch.from_numpy(off.astype(np.uint32).view(np.int32)).to(dev)
+    d_ps = torch.empty(n, dtype=torch.int32, device=dev)
+    d_po = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    times = {}
+    results = {}
+    for name in ("groups", "positions"):
+        d_ps.fill_(-1)
+        d_po.fill_(-1)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        if name == "groups":
+            ev.eval_groups_device(d_pos.data_ptr(), d_off.data_ptr(), ng, n, F.GROUP_STAR,
+                                  d_ps.data_ptr(), d_po.data_ptr(), stream)
+        else:
+            ev.eval_positions_device(d_pos.data_ptr(), n, d_ps.data_ptr(), d_po.data_ptr(), stream)
+        torch.cuda.synchronize()
+        times[name] = time.perf_counter() - t
+        ev.check()
+        results[name] = (d_ps.cpu().numpy(), d_po.cpu().numpy())
+        print(f"gpu {name}: {n / times[name] / 1e6:.1f}M positions/s (one call, host-timed)", flush=True)
+    ev.close()
+    del d_pos, d_off, d_ps, d_po
+
+    gps, gpo = results["groups"]
+    sps, spo = results["positions"]
+    paths_agree = int(((gps != sps) | (gpo != spo)).sum())
+
+    on = OracleNet(data)
+    mism = 0
+    t = time.perf_counter()
+    step = 5_000_000
+    for lo in range(0, n, step):
+        hi = min(n, lo + step)
+        ops, opo, rc = on.eval_packed(pos[lo:hi], threads=threads)
+        assert rc == 0
+        mism += int(((ops != gps[lo:hi]) | (opo != gpo[lo:hi])).sum())
+        print(f"oracle {hi}/{n} mismatches so far {mism} ({time.perf_counter() - t:.0f} s)", flush=True)
+    t_oracle = time.perf_counter() - t
+
+    rec = {"workload": "BASELINE config 4: random games (seed 3, L~U[0,160]) + all legal 1-ply children, "
+                       "synthetic SFNNv5 net HD 1024",
+           "positions": n, "groups": ng, "gen_s": round(t_gen, 1),
+           "gpu_s": {k: round(v, 3) for k, v in times.items()},
+           "gpu_positions_per_s": {k: round(n / v) for k, v in times.items()},
+           "oracle_s": round(t_oracle, 1), "oracle_threads": threads,
+           "mismatches_vs_oracle": mism, "groups_vs_positions_mismatches": paths_agree}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "full_parity.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec), flush=True)
+    assert paths_agree == 0
+    assert mism == 0
