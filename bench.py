@@ -210,23 +210,41 @@ def main():
             gathered = {"positions": int(g_ps.size), "equals_sum_of_shards": bool(g_ps.size == g_po.size
                                                                                   == int(total_positions))}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle.oracle import OracleNet  # cpu_baseline leg: the oracle is the timed CPU port
+        from oracle.oracle import OracleNet  # cpu_baseline leg: oracle/nnue_cpu_simd.c is the timed CPU port
+        from oracle.oracle import lib as olib
+        isa = "AVX-512 VNNI" if olib.cpu_simd_isa512() else "AVX2"
         on = OracleNet(F.synthesize_net(args.seed, args.hd, 0))
         done, mism, t0 = 0, 0, time.perf_counter()
         chunk = 100_000
+        if off is not None:
+            gmode = F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR
+            ng = len(off) - 1
+            g_per = max(1, int(chunk * ng / npos))
+        g = 0
         while True:
-            lo = done % npos
-            hi = min(lo + chunk, npos)
-            ps, po, rc = on.eval_packed(pos[lo:hi], threads=threads)
+            if off is None:
+                lo = done % npos
+                hi = min(lo + chunk, npos)
+                ps, po, rc = on.simd_eval_packed(pos[lo:hi], threads=threads)
+            else:
+                g0, g1 = g % ng, min(g % ng + g_per, ng)
+                lo, hi = int(off[g0]), int(off[g1])
+                ps, po, rc = on.simd_eval_groups(pos[lo:hi], (off[g0:g1 + 1] - off[g0]).astype(np.uint32), gmode,
+                                                 threads=threads)
+                g += g1 - g0
             assert rc == 0
             mism += int(((ps != psqt[lo:hi]) | (po != positional[lo:hi])).sum())
             done += hi - lo
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
         cpu_el = time.perf_counter() - t0
+        how = ("from-scratch refresh per position" if off is None else
+               "incremental accumulators along the groups, refresh on own-king moves")
         cpu = {"value": done / cpu_el, "unit": "positions/s", "cores": threads, "kind": "port",
-               "sample": f"{done} positions of the same workload (from-scratch refresh per position, "
-                         f"{cpu_el:.1f} s wall on {threads} threads; oracle/nnue_oracle.c -O3 -march=x86-64-v3)"}
+               "sample": f"{done} positions of the same workload ({how}; {cpu_el:.1f} s wall on {threads} "
+                         f"threads; oracle/nnue_cpu_simd.c = Stockfish's {isa} NNUE code paths restated "
+                         f"(register-tiled accumulators, maddubs/VPDPBUSD affine), -O3; bit-identical to the "
+                         f"scalar oracle)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
 
     # roofline.traffic: PMC-measured bytes per launch of the same workload, from the

@@ -40,6 +40,13 @@ def _load() -> C.CDLL:
     lib.oracle_eval_board.restype = C.c_int
     lib.oracle_eval_packed.argtypes = [vp, vp, C.c_size_t, vp, vp, C.c_int]
     lib.oracle_eval_packed.restype = C.c_int
+    lib.cpu_simd_eval_packed.argtypes = [vp, vp, C.c_size_t, vp, vp, C.c_int]
+    lib.cpu_simd_eval_packed.restype = C.c_int
+    lib.cpu_simd_eval_groups.argtypes = [vp, vp, vp, C.c_size_t, C.c_int, vp, vp, C.c_int]
+    lib.cpu_simd_eval_groups.restype = C.c_int
+    lib.cpu_simd_isa512.restype = C.c_int
+    lib.cpu_simd_set_isa.argtypes = [C.c_int]
+    lib.cpu_simd_set_isa.restype = C.c_int
     lib.oracle_eval_game.argtypes = [vp, C.c_char_p, C.c_char_p, vp, vp, C.c_long]
     lib.oracle_eval_game.restype = C.c_long
     lib.oracle_features.argtypes = [vp, C.c_int, vp]
@@ -74,6 +81,28 @@ class OracleNet:
         ps = np.zeros(n, dtype=np.int32)
         po = np.zeros(n, dtype=np.int32)
         rc = lib.oracle_eval_packed(self._h, pos.ctypes.data, n, ps.ctypes.data, po.ctypes.data, threads)
+        return ps, po, rc
+
+    def simd_eval_packed(self, pos: np.ndarray, threads: int = 1) -> tuple[np.ndarray, np.ndarray, int]:
+        """AVX2 restatement of the engine's evaluation (nnue_cpu_simd.c): the cpu_baseline."""
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, 36)
+        n = pos.shape[0]
+        ps = np.zeros(n, dtype=np.int32)
+        po = np.zeros(n, dtype=np.int32)
+        rc = lib.cpu_simd_eval_packed(self._h, pos.ctypes.data, n, ps.ctypes.data, po.ctypes.data, threads)
+        return ps, po, rc
+
+    def simd_eval_groups(self, pos: np.ndarray, off: np.ndarray, mode: int,
+                         threads: int = 1) -> tuple[np.ndarray, np.ndarray, int]:
+        """Incremental accumulators along CHAIN (mode 0) / STAR (mode 1) groups, AVX2."""
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, 36)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = pos.shape[0]
+        assert len(off) >= 1 and int(off[-1]) == n
+        ps = np.zeros(n, dtype=np.int32)
+        po = np.zeros(n, dtype=np.int32)
+        rc = lib.cpu_simd_eval_groups(self._h, pos.ctypes.data, off.ctypes.data, len(off) - 1, mode,
+                                      ps.ctypes.data, po.ctypes.data, threads)
         return ps, po, rc
 
     def eval_board(self, board: np.ndarray, stm: int) -> tuple[int, int]:

@@ -162,3 +162,42 @@ def test_oracle_game_replay_matches_batch_builder():
         ps, po, rc = on.eval_packed(pos)
         assert rc == 0
         assert np.array_equal(ps, ps_o) and np.array_equal(po, po_o)
+
+
+@pytest.fixture(params=["avx2", "avx512"])
+def simd_isa(request):
+    want = request.param == "avx512"
+    got = O.lib.cpu_simd_set_isa(int(want))
+    if want and not got:
+        pytest.skip("host has no AVX-512 VNNI")
+    yield request.param
+    O.lib.cpu_simd_set_isa(1)
+
+
+@pytest.mark.parametrize("hd,flags", [(1024, 0), (128, 0), (512, N.SYNTH_WRAP), (256, N.SYNTH_FC1_PAD),
+                                      (1536, 0)])
+def test_cpu_baseline_simd_matches_scalar_oracle(hd, flags, simd_isa):
+    """oracle/nnue_cpu_simd.c (the cpu_baseline: AVX2 / AVX-512 VNNI,
+    register-tiled refresh, incremental CHAIN/STAR updates) is bit-identical
+    to the scalar oracle."""
+    on = O.OracleNet(net_bytes(11, hd, flags))
+    pos = F.random_playouts(21, 3000, threads=4)
+    pos = np.concatenate([pos, np.stack([F.pos_from_fen(f) for f in FENS])])
+    a, b = on.eval_packed(pos, threads=4), on.simd_eval_packed(pos, threads=4)
+    assert a[2] == b[2] == 0
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    for mode, gmode in ((F.PLAYOUT_PLIES, N.GROUP_CHAIN), (F.PLAYOUT_CHILDREN, N.GROUP_STAR)):
+        g, off = F.random_playouts(22, 40, mode=mode, threads=4)
+        a, b = on.eval_packed(g, threads=4), on.simd_eval_groups(g, off, gmode, threads=4)
+        assert a[2] == b[2] == 0
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_cpu_baseline_simd_invalid_positions():
+    on = O.OracleNet(net_bytes(11, 128, 0))
+    pos = F.random_playouts(23, 20, mode=F.PLAYOUT_PLIES, threads=2)[0][:20].copy()
+    pos[5, :32] = 0  # no kings
+    ps, po, rc = on.simd_eval_groups(pos, np.array([0, 10, 20], dtype=np.uint32), N.GROUP_CHAIN)
+    a = on.eval_packed(pos)
+    assert rc != 0 and a[2] != 0
+    assert np.array_equal(ps, a[0]) and np.array_equal(po, a[1])
