@@ -425,6 +425,14 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
       const int v = bk == 0xFF ? 0 : (int)((uint32_t)psqt_part[2 * prow] - (uint32_t)psqt_part[2 * prow + 1]) / 2;
       psqt[perm ? perm[prow] : prow] = v;
     }
+    // output rows of this lane's fc_2 results (lane r16 == 0 of group g: rows 4g .. 4g+3),
+    // loaded with the tile so the stores at the end wait on nothing
+    uint32_t dst[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t q = min(p0 + 4 * g + r, n - 1);
+      dst[r] = perm ? perm[q] : q;
+    }
     uint32_t bmask = 0;
 #pragma unroll
     for (int b = 0; b < kStacks; ++b)
@@ -477,7 +485,7 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
       for (int r = 0; r < 4; ++r) {
         const int p = 4 * g + r;
         const int pb = __shfl(bk, p);
-        if (r16 == 0 && pb == b) positional[perm ? perm[p0 + p] : p0 + p] = W.b2 + part[r] + fwds[wv][p];
+        if (r16 == 0 && pb == b) positional[dst[r]] = W.b2 + part[r] + fwds[wv][p];
       }
       wave_lds_sync();
     }
