@@ -50,6 +50,7 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-api", action="store_true", help="skip timing the host-buffer entry points")
     ap.add_argument("--threads", type=int, default=0, help="host threads (0 = min(16, cpu_count))")
     ap.add_argument("--ft-impl", choices=["sliced", "gather"], default="sliced",
                     help="feature-transformer kernel for independent positions")
@@ -247,6 +248,25 @@ def main():
                          f"scalar oracle)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
 
+    # The host-buffer entry points (fnnue_eval_positions / _groups: host arrays in,
+    # host arrays out, PCIe both ways, host-side validation) — reported beside
+    # `value`, never as it (inputs resident in HBM is the contract).
+    host_api = None
+    if world == 1 and not args.no_host_api:
+        ev.set_timing(False)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if off is None:
+                hp, hq = ev.eval_positions(pos)
+            else:
+                hp, hq = ev.eval_groups(pos, off, F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR)
+        host_el = time.perf_counter() - t0
+        host_api = {"value": npos * reps / host_el, "unit": "positions/s",
+                    "same_results": bool(np.array_equal(hp, psqt) and np.array_equal(hq, positional)),
+                    "note": "host (pageable numpy) buffers through the C ABI: H2D 36 B + D2H 8 B per position "
+                            "over PCIe, host-side validation, then the same kernels"}
+
     # roofline.traffic: PMC-measured bytes per launch of the same workload, from the
     # committed profile (tools/profile.sh + tools/traffic.py -> profiles/traffic.json).
     traffic, traffic_src, issue = None, None, None
@@ -309,6 +329,7 @@ def main():
             "cpu_baseline": cpu,
             "parity_spot_check": parity,
             "gathered": gathered,
+            "host_api": host_api,
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
         print(json.dumps(out), flush=True)

@@ -303,7 +303,7 @@ typedef struct {
 
 static void *s_worker(void *arg) {
     s_job *j = (s_job *)arg;
-    s_state *st = (s_state *)aligned_alloc(64, 2 * sizeof(s_state));
+    s_state *st = (s_state *)aligned_alloc(64, (2 * sizeof(s_state) + 63) & ~(size_t)63);
     if (!st) { j->rc = -2; return NULL; }
     int bad = 0;
     if (!j->off) {

@@ -1,0 +1,34 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (SURVEY.md §5:
+"ASan/UBSan on the CPU oracle"): the product's .nnue parser / writer /
+generator and board code, and both CPU restatements (scalar oracle, SIMD
+baseline), built with gcc -fsanitize=address,undefined and driven by
+tests/sanitize/san_main.cpp on valid and corrupt inputs.  CPU only."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1",
+       "-march=x86-64-v3"]
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or shutil.which("gcc") is None, reason="needs gcc/g++")
+def test_host_code_under_asan_ubsan(tmp_path):
+    out = tmp_path / "san_main"
+    objs = []
+    for src in ("oracle/nnue_oracle.c", "oracle/nnue_cpu_simd.c"):
+        o = tmp_path / (os.path.basename(src) + ".o")
+        subprocess.run(["gcc", "-std=c11", *SAN, "-c", os.path.join(ROOT, src), "-o", str(o)], check=True)
+        objs.append(str(o))
+    subprocess.run(["g++", "-std=c++17", *SAN, os.path.join(ROOT, "tests/sanitize/san_main.cpp"),
+                    os.path.join(ROOT, "fishnet_amd/csrc/net.cpp"), os.path.join(ROOT, "fishnet_amd/csrc/board.cpp"),
+                    *objs, "-lpthread", "-o", str(out)], check=True)
+    # verify_asan_link_order=0: the environment may preload a library ahead of the ASan runtime
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([str(out)], capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "sanitized host checks ok" in r.stdout

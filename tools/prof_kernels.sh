@@ -7,7 +7,7 @@ tag=$1; shift
 out=$PWD/gpurun_out/pk/$tag
 mkdir -p "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > "$out/log" 2>&1 || exit 3
+  python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api "$@" > "$out/log" 2>&1 || exit 3
 python3 - "$out/run_kernel_stats.csv" "$tag" <<'PY'
 import csv, re, sys
 parts = []

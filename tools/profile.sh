@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -z "${SKIP_TRACE:-}" ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > "$OUT/trace.log" 2>&1
+    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api "$@" > "$OUT/trace.log" 2>&1
   rc=$?
   echo "trace rc=$rc"
   [ $rc -eq 0 ] || exit $rc
@@ -21,7 +21,7 @@ IFS='|' read -ra SETS <<< "$PMCS"
 for pmc in "${SETS[@]}"; do
   name=$(echo "$pmc" | tr ' ' '_' | cut -c1-60)
   timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d "$OUT/pmc_$name" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > "$OUT/pmc_$name.log" 2>&1
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-api "$@" > "$OUT/pmc_$name.log" 2>&1
   rc=$?
   echo "pmc [$pmc] rc=$rc"
   # a counter the hardware rejects fails fast (rc 1); anything else ends the run
