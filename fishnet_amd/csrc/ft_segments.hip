@@ -300,17 +300,7 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     e[4 * m + 3] = v.w;
   }
   u16x4 lo = b_lo, hi = b_hi;
-  switch ((maxn + 2) >> 2) {
-    case 1: rows_pipelined<1>(e, lbase, lo, hi); break;
-    case 2: rows_pipelined<2>(e, lbase, lo, hi); break;
-    case 3: rows_pipelined<3>(e, lbase, lo, hi); break;
-    case 4: rows_pipelined<4>(e, lbase, lo, hi); break;
-    case 5: rows_pipelined<5>(e, lbase, lo, hi); break;
-    case 6: rows_pipelined<6>(e, lbase, lo, hi); break;
-    case 7: rows_pipelined<7>(e, lbase, lo, hi); break;
-    case 8: rows_pipelined<8>(e, lbase, lo, hi); break;
-    default: break;
-  }
+  rows_sum((int)maxn - 1, e, lbase, lo, hi);
   const uint32_t col = 32 * s + 4 * q;
   __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc,
                                         ((rec.x & kSlotMask) * 2 + ((rec.x >> 24) & 1)) * (HD / 2) + col, 0, 0);

@@ -139,17 +139,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     e[4 * m + 3] = v.w;
   }
   u16x4 lo = b_lo, hi = b_hi;
-  switch ((maxn + 2) >> 2) {  // maxn - 1 rows (own king in the bias); wave-uniform, straight-line cases
-    case 1: rows_pipelined<1>(e, base, lo, hi); break;
-    case 2: rows_pipelined<2>(e, base, lo, hi); break;
-    case 3: rows_pipelined<3>(e, base, lo, hi); break;
-    case 4: rows_pipelined<4>(e, base, lo, hi); break;
-    case 5: rows_pipelined<5>(e, base, lo, hi); break;
-    case 6: rows_pipelined<6>(e, base, lo, hi); break;
-    case 7: rows_pipelined<7>(e, base, lo, hi); break;
-    case 8: rows_pipelined<8>(e, base, lo, hi); break;
-    default: break;
-  }
+  rows_sum(maxn - 1, e, base, lo, hi);  // maxn - 1 rows (own king in the bias); wave-uniform, straight-line cases
   // (rec & 0xFFFFFF) = 2 * slot + half: times HD/2 it is the offset of the
   // item's half of row `slot` of x.
   const uint32_t xoff = (rec & 0xFFFFFFu) * (HD / 2) + 32 * s + 4 * q;

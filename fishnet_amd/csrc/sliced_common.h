@@ -353,9 +353,6 @@ __device__ __forceinline__ PassFetch fetch_pass(__amdgpu_buffer_rsrc_t items, __
   return f;
 }
 
-// Reads the LDS tile rows of feature-list entries 4G .. 4G+3 (each lane its
-// 16-byte chunk q of the row).
-
 // LDS byte address of this lane's chunk of the row named by the low / high u16
 // entry of `word`: base (= plane q) + entry; hipcc emits one v_add_u32_sdwa.
 __device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word, int t) {
@@ -363,80 +360,63 @@ __device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word
   return static_cast<const u32x4*>(__builtin_assume_aligned(base + entry, 16));
 }
 
-template <int G>
-__device__ __forceinline__ void issue_rows(const uint32_t (&e)[16], const char* base, u32x4 (&v)[4]) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    v[t] = *row_addr(base, e[2 * G + (t >> 1)], t);
-#ifdef FT_EXP_DUPREAD
-    const u32x4 extra = *(row_addr(base, e[2 * G + (t >> 1)], t) + 1);
-    uint32_t sink;
-    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(sink) : "v"(extra.x), "v"(extra.y));
-#endif
-  }
-}
-
-__device__ __forceinline__ void accum_rows(const u32x4 (&v)[4], u16x4& lo, u16x4& hi) {
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    // Swizzles go through named temporaries: __builtin_bit_cast of a swizzle
-    // lvalue (v.zw) reads from the vector's base address in this clang.
-    const u32x2 a = __builtin_shufflevector(v[t], v[t], 0, 1);
-    const u32x2 b = __builtin_shufflevector(v[t], v[t], 2, 3);
-    lo += __builtin_bit_cast(u16x4, a);
-#ifdef FT_EXP_EXTRAVALU
-    {
-      uint32_t sink;
-      asm volatile("v_xor_b32 %0, %1, %2" : "=v"(sink) : "v"(a.x), "v"(b.y));
-    }
-#endif
-#ifdef FT_EXP_DUPADD
-    {
-      uint32_t s0, s1, s2, s3;
-      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s0) : "v"(a.x), "v"(a.y));
-      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s1) : "v"(a.y), "v"(b.x));
-      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s2) : "v"(b.x), "v"(b.y));
-      asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(s3) : "v"(b.y), "v"(a.x));
-    }
-#endif
-#ifndef FT_EXP_LO_ONLY
-    hi += __builtin_bit_cast(u16x4, b);
-#endif
-  }
-}
-
 #ifndef FT_DEPTH
 #define FT_DEPTH 3
 #endif
-constexpr int kDepth = FT_DEPTH;  // row groups (of 4) in flight per wave
+// Rows in flight per wave: the LDS queue stays fed and hipcc counts lgkmcnt
+// instead of draining it.
+constexpr int kRowDepth = 4 * FT_DEPTH;
 
-// NG groups of 4 rows, kDepth groups in flight, no branches: the LDS queue
-// stays fed and hipcc can count lgkmcnt instead of draining it.
-template <int NG, int G = 0>
-__device__ __forceinline__ void rows_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kDepth][4],
-                                          u16x4& lo, u16x4& hi) {
-  if constexpr (G < NG) {
-    accum_rows(v[G % kDepth], lo, hi);
-    if constexpr (G + kDepth < NG) issue_rows<G + kDepth>(e, base, v[G % kDepth]);
-    rows_step<NG, G + 1>(e, base, v, lo, hi);
+__device__ __forceinline__ void accum_row(const u32x4& v, u16x4& lo, u16x4& hi) {
+  const u32x2 a = __builtin_shufflevector(v, v, 0, 1);
+  const u32x2 b = __builtin_shufflevector(v, v, 2, 3);
+  lo += __builtin_bit_cast(u16x4, a);
+  hi += __builtin_bit_cast(u16x4, b);
+}
+
+template <int NR, int R = 0>
+__device__ __forceinline__ void rows1_head(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kRowDepth]) {
+  if constexpr (R < NR && R < kRowDepth) {
+    v[R] = *row_addr(base, e[R >> 1], R & 1);
+    rows1_head<NR, R + 1>(e, base, v);
   }
 }
 
-template <int NG, int G = 0>
-__device__ __forceinline__ void rows_issue_head(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kDepth][4]) {
-  if constexpr (G < NG && G < kDepth) {
-    issue_rows<G>(e, base, v[G]);
-    rows_issue_head<NG, G + 1>(e, base, v);
+template <int NR, int R = 0>
+__device__ __forceinline__ void rows1_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kRowDepth],
+                                           u16x4& lo, u16x4& hi) {
+  if constexpr (R < NR) {
+    accum_row(v[R % kRowDepth], lo, hi);
+    if constexpr (R + kRowDepth < NR) v[R % kRowDepth] = *row_addr(base, e[(R + kRowDepth) >> 1], (R + kRowDepth) & 1);
+    rows1_step<NR, R + 1>(e, base, v, lo, hi);
   }
 }
 
-template <int NG>
-__device__ __forceinline__ void rows_pipelined(const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
-#ifndef FT_EXP_NO_ROWS
-  u32x4 v[kDepth][4];
-  rows_issue_head<NG>(e, base, v);
-  rows_step<NG>(e, base, v, lo, hi);
-#endif
+// Exactly NR rows (a pass's longest list, not rounded up: rounding to groups of
+// 4 cost 7 % padding rows, 2 % of the kernel), kRowDepth rows in flight,
+// branch-free straight-line code per row count.
+template <int NR>
+__device__ __forceinline__ void rows_exact(const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
+  u32x4 v[kRowDepth];
+  rows1_head<NR>(e, base, v);
+  rows1_step<NR>(e, base, v, lo, hi);
+}
+
+// Sums the first `nrows` (wave-uniform, <= 32) rows of the feature list e.
+__device__ __forceinline__ void rows_sum(int nrows, const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
+  switch (nrows) {
+#define FNNUE_ROWS_CASE(k) \
+  case k: rows_exact<k>(e, base, lo, hi); break;
+    FNNUE_ROWS_CASE(1) FNNUE_ROWS_CASE(2) FNNUE_ROWS_CASE(3) FNNUE_ROWS_CASE(4) FNNUE_ROWS_CASE(5)
+    FNNUE_ROWS_CASE(6) FNNUE_ROWS_CASE(7) FNNUE_ROWS_CASE(8) FNNUE_ROWS_CASE(9) FNNUE_ROWS_CASE(10)
+    FNNUE_ROWS_CASE(11) FNNUE_ROWS_CASE(12) FNNUE_ROWS_CASE(13) FNNUE_ROWS_CASE(14) FNNUE_ROWS_CASE(15)
+    FNNUE_ROWS_CASE(16) FNNUE_ROWS_CASE(17) FNNUE_ROWS_CASE(18) FNNUE_ROWS_CASE(19) FNNUE_ROWS_CASE(20)
+    FNNUE_ROWS_CASE(21) FNNUE_ROWS_CASE(22) FNNUE_ROWS_CASE(23) FNNUE_ROWS_CASE(24) FNNUE_ROWS_CASE(25)
+    FNNUE_ROWS_CASE(26) FNNUE_ROWS_CASE(27) FNNUE_ROWS_CASE(28) FNNUE_ROWS_CASE(29) FNNUE_ROWS_CASE(30)
+    FNNUE_ROWS_CASE(31) FNNUE_ROWS_CASE(32)
+#undef FNNUE_ROWS_CASE
+    default: break;
+  }
 }
 
 }  // namespace
