@@ -440,7 +440,9 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
     v4i a[KS];
     const v4i* xr = reinterpret_cast<const v4i*>(x + (size_t)(row_ok ? prow : p0) * HD);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) a[s] = row_ok ? xr[4 * s + g] : (v4i)0;
+    // x is read exactly once: non-temporal loads (-1 %; non-temporal STORES of x
+    // in the FT cost +3 % there and +6 % here, x then misses the Infinity Cache)
+    for (int s = 0; s < KS; ++s) a[s] = row_ok ? __builtin_nontemporal_load(xr + 4 * s + g) : (v4i)0;
     while (bmask) {
       const int b = __builtin_ctz(bmask);
       bmask &= bmask - 1;
