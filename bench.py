@@ -265,7 +265,7 @@ def main():
         host_api = {"value": npos * reps / host_el, "unit": "positions/s",
                     "same_results": bool(np.array_equal(hp, psqt) and np.array_equal(hq, positional)),
                     "note": "host (pageable numpy) buffers through the C ABI: H2D 36 B + D2H 8 B per position "
-                            "over PCIe, host-side validation, then the same kernels"}
+                            "over PCIe around the same kernels (validity checked on the device)"}
 
     # roofline.traffic: PMC-measured bytes per launch of the same workload, from the
     # committed profile (tools/profile.sh + tools/traffic.py -> profiles/traffic.json).

@@ -212,6 +212,15 @@ bool valid_host_pos(const fnnue_pos& p) {
   return wk == 1 && bk == 1 && n <= 32 && p.stm <= 1;
 }
 
+// After the device latched FNNUE_E_POSITION: the message names the first
+// invalid position (the host rule is the device's, valid_host_pos).
+int name_invalid(int rc, const fnnue_pos* pos, size_t n) {
+  if (rc != FNNUE_E_POSITION) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!valid_host_pos(pos[i])) return fail(FNNUE_E_POSITION, "invalid position at index " + std::to_string(i));
+  return rc;
+}
+
 // Derives the LDS-tile layout of the FT weights from the (just uploaded) image.
 int finish_upload(fnnue_ctx* c) {
   if (std::getenv("FNNUE_DEBUG_SKIP_RELAYOUT")) {  // diagnostics only: gather path without tiles
@@ -525,8 +534,8 @@ int fnnue_eval_positions(fnnue_ctx* ctx, const fnnue_pos* pos, size_t n, int32_t
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
   if (n == 0) return FNNUE_OK;
   if (!pos || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
-  for (size_t i = 0; i < n; ++i)
-    if (!valid_host_pos(pos[i])) return fail(FNNUE_E_POSITION, "invalid position at index " + std::to_string(i));
+  // Positions are validated on the device (latched error word): the host
+  // scans them only to name the first bad index once an error is latched.
   DeviceGuard g(ctx->device);
   const size_t step = std::min<size_t>(n, 4 * (size_t)ctx->chunk);
   int rc = ensure_stage(ctx, step, 0);
@@ -540,7 +549,7 @@ int fnnue_eval_positions(fnnue_ctx* ctx, const fnnue_pos* pos, size_t n, int32_t
     HIP_TRY(hipMemcpyAsync(positional + b, ctx->d_positional, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
     rc = latched(ctx);
-    if (rc) return rc;
+    if (rc) return name_invalid(rc, pos, n);
   }
   return FNNUE_OK;
 }
@@ -555,8 +564,6 @@ int fnnue_eval_groups(fnnue_ctx* ctx, const fnnue_pos* pos, const uint32_t* off,
   for (size_t g = 0; g < ngroups; ++g)
     if (off[g + 1] < off[g]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
   const size_t npos = off[ngroups];
-  for (size_t i = 0; i < npos; ++i)
-    if (!valid_host_pos(pos[i])) return fail(FNNUE_E_POSITION, "invalid position at index " + std::to_string(i));
   DeviceGuard g(ctx->device);
   int rc = ensure_stage(ctx, std::max<size_t>(npos, 1), ngroups + 1);
   if (rc) return rc;
@@ -568,7 +575,7 @@ int fnnue_eval_groups(fnnue_ctx* ctx, const fnnue_pos* pos, const uint32_t* off,
   HIP_TRY(hipMemcpyAsync(psqt, ctx->d_psqt, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
   HIP_TRY(hipMemcpyAsync(positional, ctx->d_positional, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
   HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-  return latched(ctx);
+  return name_invalid(latched(ctx), pos, npos);
 }
 
 // ---- batch building ----

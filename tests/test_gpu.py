@@ -137,6 +137,7 @@ def test_invalid_position_fails_whole_batch(ev_cache):
     with pytest.raises(F.FnnueError) as e:
         ev.eval_positions(pos)
     assert e.value.name == "FNNUE_E_POSITION"
+    assert "index 3" in str(e.value)  # latched on the device, named by the host
     pos = F.random_playouts(5, 10, threads=2)
     pos[4, 0] = (pos[4, 0] & 0xF0) | 7  # invalid piece code 7 on a1
     with pytest.raises(F.FnnueError) as e:

@@ -23,7 +23,7 @@ import sys
 
 prof, key = sys.argv[1], sys.argv[2]
 pat = re.compile(sys.argv[3] if len(sys.argv) > 3 else r"plan_|ft_slices|ft_scratch|ft_groups")
-dominant = re.compile(r"ft_slices|ft_scratch|ft_groups")
+dominant = re.compile(r"ft_slices|ft_segments|ft_scratch|ft_groups")
 per_kernel = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{prof}/pmc_*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
