@@ -103,6 +103,9 @@ int fnnue_ctx_image(fnnue_ctx *ctx, const void **device_image, size_t *bytes);
 void fnnue_ctx_free(fnnue_ctx *ctx);
 
 /* ---- evaluation, host buffers (synchronous) ----
+ * Copies in, runs the device path, copies out.  Position validity is checked
+ * on the device; an invalid position fails the whole call with
+ * FNNUE_E_POSITION (message: its index) and no outputs are guaranteed.
  * Static eval of independent positions, accumulators from scratch.  Replaces
  * one `position fen ... ` + eval round trip per position ([ref]
  * src/stockfish.rs:274-283 / StockfishStub::go :44-54) with one batched call. */
