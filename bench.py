@@ -15,6 +15,7 @@ rank 0 once at start-up.
 Other workloads (not the headline line; the other BASELINE configs, measured for DESIGN.md):
   --workload games     config 3: random-playout games, every ply, incremental (CHAIN)
   --workload children  config 4: every ply of random games plus all legal children (STAR)
+  --small-net 128      also evaluate every position with a small net each step (config 3's big + small)
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -47,6 +48,9 @@ def parse_args():
     ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions workload)")
     ap.add_argument("--games", type=int, default=10_000, help="games per GPU (games / children workloads)")
     ap.add_argument("--hd", type=int, default=1024)
+    ap.add_argument("--small-net", type=int, default=0, metavar="HD",
+                    help="also evaluate every position with a second (small) net of this width each step "
+                         "(BASELINE config 3: big + small net; later Stockfish's small net is HD 128)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -111,6 +115,14 @@ def main():
     ev = F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=args.hd)
     ev.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
     del img
+    ev_small = None
+    if args.small_net:
+        image2 = (F.Net.from_bytes(F.synthesize_net(args.seed + 1000, args.small_net, 0)).image()
+                  if rank == 0 else None)
+        img2 = D.broadcast_image(image2, dev) if dist_on else torch.from_numpy(image2).to(dev)
+        torch.cuda.synchronize()
+        ev_small = F.Evaluator(None, local, image_ptr=img2.data_ptr(), image_bytes=img2.numel(), hd=args.small_net)
+        del img2
     t_net = time.time() - t0
 
     # ---- inputs: this rank's shard, resident in HBM ----
@@ -140,6 +152,9 @@ def main():
                     % ("3" if args.workload == "games" else "4", args.games,
                        "every ply, incremental CHAIN" if args.workload == "games"
                        else "every ply + all legal 1-ply children, STAR", args.hd))
+    if args.small_net:
+        workload += (f"; every position also through a second synthetic net of HD {args.small_net} "
+                     f"(big + small net, both evaluated each step)")
     t_gen = time.time() - t0
     npos = len(pos)
     pieces = (board != 0).sum(axis=1)
@@ -147,23 +162,29 @@ def main():
     d_off = torch.from_numpy(off.astype(np.int32)).to(dev) if off is not None else None
     d_psqt = torch.zeros(npos, dtype=torch.int32, device=dev)
     d_positional = torch.zeros(npos, dtype=torch.int32, device=dev)
+    d_small = torch.zeros(2, npos, dtype=torch.int32, device=dev) if ev_small else None
     stream = torch.cuda.current_stream()
 
-    if off is None:
-        def step():
-            ev.eval_positions_device(d_pos.data_ptr(), npos, d_psqt.data_ptr(), d_positional.data_ptr(),
-                                     stream.cuda_stream)
-    else:
-        gmode = F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR
+    def run(e, ps, po):
+        if off is None:
+            e.eval_positions_device(d_pos.data_ptr(), npos, ps, po, stream.cuda_stream)
+        else:
+            e.eval_groups_device(d_pos.data_ptr(), d_off.data_ptr(), len(off) - 1, npos,
+                                 F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR, ps, po,
+                                 stream.cuda_stream)
 
-        def step():
-            ev.eval_groups_device(d_pos.data_ptr(), d_off.data_ptr(), len(off) - 1, npos, gmode,
-                                  d_psqt.data_ptr(), d_positional.data_ptr(), stream.cuda_stream)
+    def step():
+        run(ev, d_psqt.data_ptr(), d_positional.data_ptr())
+        if ev_small:
+            run(ev_small, d_small[0].data_ptr(), d_small[1].data_ptr())
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     ev.check()
+    if ev_small:
+        ev_small.check()
+        ev_small.set_timing(True)
 
     ev.set_timing(True)
     if dist_on:
@@ -179,6 +200,21 @@ def main():
     launches, ft_ms, stack_ms = ev.timing_read()
     ev.set_timing(False)
     ev.check()
+    small = None
+    if ev_small:
+        l2, f2, s2 = ev_small.timing_read()
+        ev_small.set_timing(False)
+        ev_small.check()
+        # parity of the small net on a bounded sample against the oracle (test infrastructure)
+        from oracle.oracle import OracleNet
+        on2 = OracleNet(F.synthesize_net(args.seed + 1000, args.small_net, 0))
+        k = min(npos, 200_000)
+        ps2, po2, rc2 = on2.simd_eval_packed(pos[:k], threads=threads)
+        g2 = d_small[:, :k].cpu().numpy()
+        small = {"hd": args.small_net, "ft_kernel_avg_ms": round(f2 / max(l2, 1), 4),
+                 "stack_kernel_avg_ms": round(s2 / max(l2, 1), 4),
+                 "parity_spot_check": {"checked": k, "mismatches": int(((g2[0] != ps2) | (g2[1] != po2)).sum())
+                                       if rc2 == 0 else None}}
     if dist_on:
         elapsed_max = D.max_over_ranks(elapsed, dev)
         tot = torch.tensor([float(npos)], dtype=torch.float64, device=dev)
@@ -304,7 +340,7 @@ def main():
                 "workload": workload,
                 "positions_per_gpu": npos,
                 "mean_pieces": round(float(pieces.mean()), 3),
-                "hd": args.hd,
+                "hd": args.hd if not args.small_net else f"{args.hd}+{args.small_net}",
                 "parallelism": f"dp{world}",
                 "ft_impl": args.ft_impl if off is None else "groups",
             },
@@ -330,10 +366,13 @@ def main():
             "parity_spot_check": parity,
             "gathered": gathered,
             "host_api": host_api,
+            "small_net": small,
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
         print(json.dumps(out), flush=True)
     ev.close()
+    if ev_small:
+        ev_small.close()
     if dist_on:
         dist.destroy_process_group()
 

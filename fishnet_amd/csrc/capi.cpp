@@ -193,6 +193,7 @@ int latched(fnnue_ctx* c) {
   HIP_TRY(hipMemcpy(&h, c->err, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy(error word)");
   if (h) {
     HIP_TRY(hipMemset(c->err, 0, sizeof(uint32_t)), "hipMemset");
+    if (h & 2u) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing and span [0, npos)");
     return fail(FNNUE_E_POSITION, "batch contains an invalid position (needs one king per side, <= 32 pieces, "
                                   "valid piece codes, stm 0/1)");
   }
@@ -486,8 +487,20 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   if (ctx->ft_impl == FNNUE_FT_SLICED) {
-    const int rc = ensure_seg(ctx);
+    int rc = ensure_seg(ctx);
     if (rc) return rc;
+    if (npos <= ctx->chunk) {
+      // One launch: the offsets never come to the host (no D2H round trip and
+      // no stream drain per call); they are checked on the device instead.
+      std::array<hipEvent_t, 3>* ev = nullptr;
+      if ((rc = next_events(ctx, &ev))) return rc;
+      if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+      HIP_TRY(launch_groups_check(d_off, (uint32_t)ngroups, (uint32_t)npos, ctx->err, s), "offset check launch");
+      HIP_TRY(launch_ft_segments(ctx->hd, d_pos, (uint32_t)npos, d_off, (uint32_t)ngroups, 0, mode, ctx->ptrs,
+                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s),
+              "ft_segments launch");
+      return run_chunk_tail(ctx, (uint32_t)npos, d_positional, s, ev, nullptr, ctx->plan.psqt_part, d_psqt);
+    }
   }
   std::vector<uint32_t> off(ngroups + 1);
   HIP_TRY(hipMemcpyAsync(off.data(), d_off, off.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpy");

@@ -42,20 +42,36 @@ constexpr uint32_t kSlotMask = 0xFFFFFF;  // record x: slot | half << 24 | bucke
 // A segment item is a whole run of positions walked serially, so units are
 // cut by positions (kSegUnitPlies, plan_scan_kernel) rather than by items.
 
-// The group of position i (chunk-relative): its first position and its end.
+// The group of position i (chunk-relative): its first position and its end,
+// clamped to first <= i < end <= n.  With valid offsets the clamp is a no-op;
+// with malformed ones (the device entry point checks them on the device,
+// groups_check_kernel) every access stays inside the chunk.  Grouping never
+// affects results: deltas are diffs of the two boards, a refresh otherwise.
 __device__ __forceinline__ uint2 group_range(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
-                                             uint32_t i) {
+                                             uint32_t i, uint32_t n) {
   uint32_t lo = 0, hi = ngroups;  // off[lo] - base <= i < off[hi] - base
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (off[mid] - base <= i) lo = mid;
     else hi = mid;
   }
-  return make_uint2(off[lo] - base, off[lo + 1] - base);
+  return make_uint2(min(off[lo] - base, i), min(max(off[lo + 1] - base, i + 1), n));
 }
 __device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
-                                                uint32_t i) {
-  return group_range(off, ngroups, base, i).x;
+                                                uint32_t i, uint32_t n) {
+  return group_range(off, ngroups, base, i, n).x;
+}
+
+// Offsets of a call the host did not read (fnnue_eval_groups_device with
+// npos <= the workspace): non-decreasing, off[0] = 0, off[ngroups] = npos,
+// else error bit 2 (FNNUE_E_ARG).
+__global__ __launch_bounds__(256) void groups_check_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                           uint32_t npos, uint32_t* __restrict__ err) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngroups) return;
+  bool bad = off[g + 1] < off[g];
+  if (g == 0) bad |= off[0] != 0 || off[ngroups] != npos;
+  if (bad) atomicOr(err, 2u);
 }
 
 __device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int ksq, int kb) {
@@ -79,7 +95,7 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
   }
   const uint32_t bk = (uint32_t)(B.cnt - 1) >> 2;
   bucket[i] = (uint8_t)bk;
-  const uint32_t first = group_first(off, ngroups, base, i);
+  const uint32_t first = group_first(off, ngroups, base, i, n);
   const bool has_base = i > first;
   LaneBoard A;
   bool base_ok = false;
@@ -144,7 +160,7 @@ __global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint32_t
   uint32_t L = 0;
   if (ref[j] && bucket[i] != 0xFF) {
     if (star) {
-      const uint2 g = group_range(off, ngroups, base, i);
+      const uint2 g = group_range(off, ngroups, base, i, n);
       L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
     } else {
       const uint32_t k = cref[j];
@@ -166,7 +182,7 @@ __global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint
   const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
   uint32_t r, rank;
   if (star) {
-    r = group_first(off, ngroups, base, i);  // the parent: a refresh item of this perspective
+    r = group_first(off, ngroups, base, i, n);  // the parent: a refresh item of this perspective
     rank = (i - r) - (cref[j] - cref[c * n + r + 1]);
   } else {
     r = ipos[cref[j] - 1];  // the last refresh of this perspective before i (same game)
@@ -500,6 +516,13 @@ size_t seg_scan_temp_bytes(uint32_t chunk) {
     case 3072: return CALL(3072);   \
     default: return hipErrorInvalidValue; \
   }
+
+hipError_t launch_groups_check(const uint32_t* off, uint32_t ngroups, uint32_t npos, uint32_t* err,
+                               hipStream_t stream) {
+  if (ngroups == 0) return hipSuccess;
+  hipLaunchKernelGGL(groups_check_kernel, dim3((ngroups + 255) / 256), dim3(256), 0, stream, off, ngroups, npos, err);
+  return hipGetLastError();
+}
 
 hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
                               uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,

@@ -300,3 +300,36 @@ def test_groups_device_latched_invalid(ev_cache):
         ok[holes] = False
         assert np.all(ps[~ok] == 0) and np.all(po[~ok] == 0)
         assert np.array_equal(ps[ok], ops[ok]) and np.array_equal(po[ok], opo[ok])
+
+
+def test_device_groups_offsets_checked_on_device(ev_cache):
+    """fnnue_eval_groups_device never reads the offsets on the host (one launch):
+    malformed offsets latch FNNUE_E_ARG, stay in bounds, and the ctx stays usable;
+    arbitrary (valid) groupings give the oracle's results."""
+    import torch
+    ev, on = ev_cache()
+    pos, off = F.random_playouts(31, 40, mode=F.PLAYOUT_PLIES, threads=2)
+    n = len(pos)
+    d = torch.from_numpy(pos).cuda()
+    ps = torch.zeros(n, dtype=torch.int32, device="cuda")
+    po = torch.zeros(n, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for bad in ([0, 50, 20, n], [0, 10, n - 1], [5, 10, n], [0, n + 7]):
+        d_off = torch.tensor(bad, dtype=torch.int32, device="cuda")
+        for mode in (F.GROUP_CHAIN, F.GROUP_STAR):
+            ev.eval_groups_device(d.data_ptr(), d_off.data_ptr(), len(bad) - 1, n, mode, ps.data_ptr(),
+                                  po.data_ptr(), stream)
+            with pytest.raises(F.FnnueError) as e:
+                ev.check()
+            assert e.value.name == "FNNUE_E_ARG"
+    ops, opo, rc = on.eval_packed(pos, threads=4)
+    assert rc == 0
+    # valid but arbitrary groupings: STAR "children" that are other plies, CHAIN cut mid-game
+    rng = np.random.default_rng(3)
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n, 57)])).astype(np.uint32)
+    for mode in (F.GROUP_CHAIN, F.GROUP_STAR):
+        d_off = torch.from_numpy(cuts.view(np.int32)).cuda()
+        ev.eval_groups_device(d.data_ptr(), d_off.data_ptr(), len(cuts) - 1, n, mode, ps.data_ptr(), po.data_ptr(),
+                              stream)
+        ev.check()
+        assert np.array_equal(ps.cpu().numpy(), ops) and np.array_equal(po.cpu().numpy(), opo)
