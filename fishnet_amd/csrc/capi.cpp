@@ -106,7 +106,7 @@ void ctx_destroy(fnnue_ctx* c) {
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
                   (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm,
                   (void*)c->plan.psqt_part, (void*)c->seg.ref, (void*)c->seg.cref, c->seg.dtmp, c->seg.drec,
-                  (void*)c->seg.ipos, (void*)c->seg.len, c->seg.items, c->seg.scan_temp})
+                  (void*)c->seg.ipos, (void*)c->seg.len, c->seg.items, c->seg.span, c->seg.scan_temp})
     if (p) (void)hipFree(p);
   delete c;
 }
@@ -254,7 +254,8 @@ int ensure_seg(fnnue_ctx* c) {
   if (hipMalloc(&G.ref, (n2 + 1) * 4) != hipSuccess || hipMalloc(&G.cref, (n2 + 1) * 4) != hipSuccess ||
       hipMalloc(&G.dtmp, n2 * 16) != hipSuccess || hipMalloc(&G.drec, n2 * 16) != hipSuccess ||
       hipMalloc(&G.ipos, n2 * 4) != hipSuccess || hipMalloc(&G.len, n2 * 4) != hipSuccess ||
-      hipMalloc(&G.items, n2 * 16) != hipSuccess || hipMalloc(&G.scan_temp, G.scan_temp_bytes + 16) != hipSuccess)
+      hipMalloc(&G.items, n2 * 16) != hipSuccess || hipMalloc(&G.span, (size_t)c->chunk * 8) != hipSuccess ||
+      hipMalloc(&G.scan_temp, G.scan_temp_bytes + 16) != hipSuccess)
     return fail(FNNUE_E_OOM, "device allocation (segment plan)");
   return FNNUE_OK;
 }

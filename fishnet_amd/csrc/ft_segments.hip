@@ -17,6 +17,7 @@
 // wrap is a group, so results equal a refresh bit for bit.
 //
 // Plan (all on the device, per chunk of positions):
+//   group_span    per position its group's {first, end} (thread per group)
 //   seg_delta     per (position, perspective): refresh flag or the delta
 //                 record {slot, half, bucket, 2 removed, 2 added rows}
 //   scan          exclusive scan of refresh flags -> item index per refresh
@@ -42,24 +43,25 @@ constexpr uint32_t kSlotMask = 0xFFFFFF;  // record x: slot | half << 24 | bucke
 // A segment item is a whole run of positions walked serially, so units are
 // cut by positions (kSegUnitPlies, plan_scan_kernel) rather than by items.
 
-// The group of position i (chunk-relative): its first position and its end,
-// clamped to first <= i < end <= n.  With valid offsets the clamp is a no-op;
-// with malformed ones (the device entry point checks them on the device,
+// Each position's group span {first, end} (chunk-relative), written by
+// group_span_kernel: one wave per group fills its members (coalesced), so the
+// plan kernels read one word pair instead of binary-searching the offsets.
+__global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                         uint32_t base, uint32_t n, uint2* __restrict__ span) {
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  const uint32_t a = min(off[g] - base, n), b = min(max(off[g + 1] - base, a), n);
+  for (uint32_t i = a + (threadIdx.x & 63); i < b; i += 64) span[i] = make_uint2(a, b);
+}
+
+// The group of position i, clamped to first <= i < end <= n.  With valid
+// offsets the clamp is a no-op; with malformed ones (gaps leave span entries
+// unwritten; the device entry point checks offsets on the device,
 // groups_check_kernel) every access stays inside the chunk.  Grouping never
 // affects results: deltas are diffs of the two boards, a refresh otherwise.
-__device__ __forceinline__ uint2 group_range(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
-                                             uint32_t i, uint32_t n) {
-  uint32_t lo = 0, hi = ngroups;  // off[lo] - base <= i < off[hi] - base
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (off[mid] - base <= i) lo = mid;
-    else hi = mid;
-  }
-  return make_uint2(min(off[lo] - base, i), min(max(off[lo + 1] - base, i + 1), n));
-}
-__device__ __forceinline__ uint32_t group_first(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t base,
-                                                uint32_t i, uint32_t n) {
-  return group_range(off, ngroups, base, i, n).x;
+__device__ __forceinline__ uint2 group_range(const uint2* __restrict__ span, uint32_t i, uint32_t n) {
+  const uint2 v = span[i];
+  return make_uint2(min(v.x, i), min(max(v.y, i + 1), n));
 }
 
 // Offsets of a call the host did not read (fnnue_eval_groups_device with
@@ -79,8 +81,8 @@ __device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int 
 }
 
 __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                                        const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                        uint32_t base, int star, uint32_t* __restrict__ ref,
+                                                        const uint2* __restrict__ span, int star,
+                                                        uint32_t* __restrict__ ref,
                                                         uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
                                                         uint32_t* __restrict__ err) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
   }
   const uint32_t bk = (uint32_t)(B.cnt - 1) >> 2;
   bucket[i] = (uint8_t)bk;
-  const uint32_t first = group_first(off, ngroups, base, i, n);
+  const uint32_t first = group_range(span, i, n).x;
   const bool has_base = i > first;
   LaneBoard A;
   bool base_ok = false;
@@ -149,8 +151,8 @@ __global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint32
 // Segment length at each valid refresh (0 elsewhere).  CHAIN: up to the next
 // refresh of the same perspective (the next item; groups start with one).
 // STAR: the group's parent owns its children that are not refreshes.
-__global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                      uint32_t base, int star, const uint8_t* __restrict__ bucket,
+__global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint2* __restrict__ span, int star,
+                                                      const uint8_t* __restrict__ bucket,
                                                       const uint32_t* __restrict__ ref,
                                                       const uint32_t* __restrict__ cref,
                                                       const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len) {
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint32_t
   uint32_t L = 0;
   if (ref[j] && bucket[i] != 0xFF) {
     if (star) {
-      const uint2 g = group_range(off, ngroups, base, i, n);
+      const uint2 g = group_range(span, i, n);
       L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
     } else {
       const uint32_t k = cref[j];
@@ -170,8 +172,7 @@ __global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint32_t
   len[j] = L;
 }
 
-__global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint32_t* __restrict__ off,
-                                                          uint32_t ngroups, uint32_t base, int star,
+__global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint2* __restrict__ span, int star,
                                                           const uint8_t* __restrict__ bucket,
                                                           const uint32_t* __restrict__ ref,
                                                           const uint32_t* __restrict__ cref,
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint
   const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
   uint32_t r, rank;
   if (star) {
-    r = group_first(off, ngroups, base, i, n);  // the parent: a refresh item of this perspective
+    r = group_range(span, i, n).x;  // the parent: a refresh item of this perspective
     rank = (i - r) - (cref[j] - cref[c * n + r + 1]);
   } else {
     r = ipos[cref[j] - 1];  // the last refresh of this perspective before i (same game)
@@ -534,7 +535,11 @@ hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, con
   // ref[2n] is followed by one zero word so the scan yields cref[2n] = item count
   if ((e = hipMemsetAsync(G.ref + 2 * (size_t)n, 0, 4, stream)) != hipSuccess) return e;
   const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
-  hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, off, ngroups, base, star ? 1 : 0, G.ref,
+  const uint2* span = reinterpret_cast<const uint2*>(G.span);
+  hipLaunchKernelGGL(group_span_kernel, dim3((ngroups + 3) / 4), dim3(256), 0, stream, off, ngroups, base, n,
+                     (uint2*)G.span);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, span, star ? 1 : 0, G.ref,
                      (uint4*)G.dtmp, bucket, err);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   size_t tb = G.scan_temp_bytes;
@@ -542,10 +547,10 @@ hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, con
     return e;
   hipLaunchKernelGGL(seg_items_kernel, dim3(g2), dim3(bs), 0, stream, n, G.ref, G.cref, G.ipos);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_len_kernel, dim3(g2), dim3(bs), 0, stream, n, off, ngroups, base, star ? 1 : 0, bucket,
+  hipLaunchKernelGGL(seg_len_kernel, dim3(g2), dim3(bs), 0, stream, n, span, star ? 1 : 0, bucket,
                      G.ref, G.cref, G.ipos, G.len);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_members_kernel, dim3(g2), dim3(bs), 0, stream, n, off, ngroups, base, star ? 1 : 0, bucket,
+  hipLaunchKernelGGL(seg_members_kernel, dim3(g2), dim3(bs), 0, stream, n, span, star ? 1 : 0, bucket,
                      G.ref, G.cref, G.ipos, (const uint4*)G.dtmp, (uint4*)G.drec);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   uint32_t cb = (2 * n + 1023) / 1024;

@@ -79,6 +79,7 @@ struct SegPlan {
   uint32_t* ipos;     // [2 * chunk] item -> root position
   uint32_t* len;      // [2 * chunk] segment length at the root
   void* items;        // uint4 [2 * chunk] sorted item records
+  void* span;         // uint2 [chunk] group {first, end} per position
   void* scan_temp;
   size_t scan_temp_bytes;
 };
