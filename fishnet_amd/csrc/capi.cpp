@@ -139,6 +139,10 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
   c->device = device;
   c->hd = hd;
   c->chunk = chunk_for_hd(hd);
+  if (const char* s = std::getenv("FNNUE_CHUNK")) {  // experiment knob: smaller launches (multiple of 1024)
+    const unsigned long v = std::strtoul(s, nullptr, 10) & ~1023ul;
+    if (v >= 1024 && v < c->chunk) c->chunk = (uint32_t)v;
+  }
   const uint32_t chunk = c->chunk;
   DeviceGuard g(device);
   c->image_bytes = image_layout(hd).total;
