@@ -31,6 +31,8 @@
 //   ft_segments   (unit, slice) workgroups, XCD-aware, tile in LDS
 // then stack_kernel over x / bucket / psqt_part in position order.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <hipcub/hipcub.hpp>
 
 #include "sliced_common.h"
@@ -275,20 +277,29 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 }
 
 // One delta position: cur = base -/+ the removed / added rows of record d.
+// kAdd2 = false when no record of the batch has a second added piece (only
+// the other side's castling has one), which skips that row.
+template <bool kAdd2>
 __device__ __forceinline__ void apply_delta(const char* lbase, const uint4& d, u16x4 b_lo, u16x4 b_hi, u16x4& lo,
                                             u16x4& hi) {
   const u32x4 r0 = *row_addr(lbase, d.y, 0), r1 = *row_addr(lbase, d.y, 1);
-  const u32x4 a0 = *row_addr(lbase, d.z, 0), a1 = *row_addr(lbase, d.z, 1);
+  const u32x4 a0 = *row_addr(lbase, d.z, 0);
   auto lo2 = [](const u32x4& v) { return __builtin_bit_cast(u16x4, __builtin_shufflevector(v, v, 0, 1)); };
   auto hi2 = [](const u32x4& v) { return __builtin_bit_cast(u16x4, __builtin_shufflevector(v, v, 2, 3)); };
-  lo = b_lo - lo2(r0) - lo2(r1) + lo2(a0) + lo2(a1);
-  hi = b_hi - hi2(r0) - hi2(r1) + hi2(a0) + hi2(a1);
+  lo = b_lo - lo2(r0) - lo2(r1) + lo2(a0);
+  hi = b_hi - hi2(r0) - hi2(r1) + hi2(a0);
+  if constexpr (kAdd2) {
+    const u32x4 a1 = *row_addr(lbase, d.z, 1);
+    lo += lo2(a1);
+    hi += hi2(a1);
+  }
 }
 
+template <bool kAdd2>
 __device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4& d, int q) {
-  auto p = [&](uint32_t e) { return ptile[(e >> 4) * kPsqtBuckets + q]; };
-  return (int32_t)((uint32_t)p(d.z & 0xFFFFu) + (uint32_t)p(d.z >> 16) - (uint32_t)p(d.y & 0xFFFFu) -
-                   (uint32_t)p(d.y >> 16));
+  auto p = [&](uint32_t e) { return (uint32_t)ptile[(e >> 4) * kPsqtBuckets + q]; };
+  const uint32_t a2 = kAdd2 ? p(d.z >> 16) : 0u;
+  return (int32_t)(p(d.z & 0xFFFFu) + a2 - p(d.y & 0xFFFFu) - p(d.y >> 16));
 }
 
 // One pass = 8 segment items per wave.  Refresh position: as slice_pass
@@ -352,22 +363,21 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   uint4 next = fetch(1 + q);
   u16x4 blo = lo, bhi = hi;
   int32_t pb = p;
-  for (uint32_t b = 0; b < nb; ++b) {
-    const uint4 batch = next;
-    next = fetch(8 * (b + 1) + 1 + q);
-    db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
+  // The 8 positions of a batch, straight-line; kAdd2 as in apply_delta.
+  auto run_batch = [&](uint32_t b, auto add2) {
+    constexpr bool kAdd2 = decltype(add2)::value;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const uint32_t k = 8 * b + 1 + jj;
       uint4 d = db[jj];
       const bool live = k < L;
       if (!live) d = make_uint4(0u, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
-      apply_delta(lbase, d, blo, bhi, lo, hi);
+      apply_delta<kAdd2>(lbase, d, blo, bhi, lo, hi);
       const uint32_t xo = live ? ((d.x & kSlotMask) * 2 + ((d.x >> 24) & 1)) * (HD / 2) + col : kDroppedOffset;
       __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
       int32_t pc = 0;
       if constexpr (kPsqt) {
-        pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta(ptile, d, q));
+        pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta<kAdd2>(ptile, d, q));
         __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, psqt_off(d.x, live), 0, 0);
       }
       if constexpr (!kStar) {
@@ -376,6 +386,16 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
         pb = pc;
       }
     }
+  };
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint4 batch = next;
+    next = fetch(8 * (b + 1) + 1 + q);
+    db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
+    // lane q of an item holds record 8b+1+q: any live one with a second add?
+    if (__ballot(8 * b + 1 + q < L && (batch.z >> 16) != kNoEntry))
+      run_batch(b, std::true_type{});
+    else
+      run_batch(b, std::false_type{});
   }
 }
 
