@@ -360,7 +360,13 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   uint4* db = dbuf + 8 * it_in_wave;
   const uint32_t L = rec.y;
   const uint32_t nb = __builtin_amdgcn_readfirstlane((maxL - 1 + 7) / 8);  // batches, wave-uniform
-  uint4 next = fetch(1 + q);
+#ifndef SEG_PREFETCH
+#define SEG_PREFETCH 1
+#endif
+  constexpr int kAhead = SEG_PREFETCH;  // batches of records in flight ahead of the current one
+  uint4 next[kAhead];
+#pragma unroll
+  for (int a = 0; a < kAhead; ++a) next[a] = fetch(8 * a + 1 + q);
   u16x4 blo = lo, bhi = hi;
   int32_t pb = p;
   // The 8 positions of a batch, straight-line; kAdd2 as in apply_delta.
@@ -388,8 +394,10 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     }
   };
   for (uint32_t b = 0; b < nb; ++b) {
-    const uint4 batch = next;
-    next = fetch(8 * (b + 1) + 1 + q);
+    const uint4 batch = next[0];
+#pragma unroll
+    for (int a = 0; a + 1 < kAhead; ++a) next[a] = next[a + 1];
+    next[kAhead - 1] = fetch(8 * (b + kAhead) + 1 + q);
     db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
     // lane q of an item holds record 8b+1+q: any live one with a second add?
     if (__ballot(8 * b + 1 + q < L && (batch.z >> 16) != kNoEntry))
