@@ -41,7 +41,8 @@ namespace fnnue {
 
 namespace {
 
-constexpr uint32_t kSlotMask = 0xFFFFFF;  // record x: slot | half << 24 | bucket << 25
+constexpr uint32_t kSlotMask = 0xFFFFFF;  // item record x: slot | half << 24 | bucket << 25
+constexpr uint32_t kRowMask = 0x1FFFFFF;  // delta record x: (2 * slot + half) | bucket << 25
 // A segment item is a whole run of positions walked serially, so units are
 // cut by positions (kSegUnitPlies, plan_scan_kernel) rather than by items.
 
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
     ref[c * n + i] = refresh ? 1u : 0u;
     if (!refresh) {
       const uint32_t half = B.stm == c ? 0u : 1u;
-      dtmp[c * n + i] = make_uint4(i | half << 24 | bk << 25, rem[0] | rem[1] << 16, add[0] | add[1] << 16, 0u);
+      dtmp[c * n + i] = make_uint4((2u * i + half) | bk << 25, rem[0] | rem[1] << 16, add[0] | add[1] << 16, 0u);
     }
   }
 }
@@ -379,12 +380,13 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
       const bool live = k < L;
       if (!live) d = make_uint4(0u, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
       apply_delta<kAdd2>(lbase, d, blo, bhi, lo, hi);
-      const uint32_t xo = live ? ((d.x & kSlotMask) * 2 + ((d.x >> 24) & 1)) * (HD / 2) + col : kDroppedOffset;
+      const uint32_t xo = live ? (d.x & kRowMask) * (HD / 2) + col : kDroppedOffset;
       __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
       int32_t pc = 0;
       if constexpr (kPsqt) {
         pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta<kAdd2>(ptile, d, q));
-        __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, psqt_off(d.x, live), 0, 0);
+        const uint32_t po = (live && (int)(d.x >> 25) == q) ? (d.x & kRowMask) * 4u : kDroppedOffset;
+        __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, po, 0, 0);
       }
       if constexpr (!kStar) {
         blo = lo;
