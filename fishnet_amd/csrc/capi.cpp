@@ -256,7 +256,7 @@ int ensure_seg(fnnue_ctx* c) {
   const size_t n2 = 2 * (size_t)c->chunk;
   G.scan_temp_bytes = seg_scan_temp_bytes(c->chunk);
   if (hipMalloc(&G.ref, (n2 + 1) * 4) != hipSuccess || hipMalloc(&G.cref, (n2 + 1) * 4) != hipSuccess ||
-      hipMalloc(&G.dtmp, n2 * 16) != hipSuccess || hipMalloc(&G.drec, n2 * 16) != hipSuccess ||
+      hipMalloc(&G.dtmp, n2 * 16) != hipSuccess || hipMalloc(&G.drec, n2 * 16 + 16) != hipSuccess ||
       hipMalloc(&G.ipos, n2 * 4) != hipSuccess || hipMalloc(&G.len, n2 * 4) != hipSuccess ||
       hipMalloc(&G.items, n2 * 16) != hipSuccess || hipMalloc(&G.span, (size_t)c->chunk * 8) != hipSuccess ||
       hipMalloc(&G.scan_temp, G.scan_temp_bytes + 16) != hipSuccess)

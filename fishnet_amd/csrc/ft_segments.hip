@@ -182,6 +182,10 @@ __global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint
                                                           const uint32_t* __restrict__ ipos,
                                                           const uint4* __restrict__ dtmp, uint4* __restrict__ drec) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  // Record 2n, read by items past the end of their segment: no rows, x row 2n
+  // and bucket 0, i.e. x and PSQT stores just past the launch's buffer ranges
+  // (dropped by the hardware), so the walk needs no liveness masking.
+  if (j == 0) drec[2 * n] = make_uint4(2 * n, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
   if (j >= 2 * n || ref[j]) return;
   const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
   uint32_t r, rank;
@@ -351,15 +355,14 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   // lane per 8 positions, the next batch prefetched) and spreads the batch
   // through the wave's LDS buffer; the 8 positions of a batch are straight-
   // line code, so their LDS reads issue ahead of the accumulator chain.
-  // Finished items (k >= L) read the zero-filled record past the buffer and
-  // are masked to the zero row with their stores dropped.
+  // Finished items (k >= L) read the sentinel record 2n: zero rows, stores
+  // past the buffer ranges (dropped).
   const uint32_t rbase = (rec.z * n + (rec.x & kSlotMask)) * 16u;
   auto fetch = [&](uint32_t k) {
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drec_rsrc, k < rec.y ? rbase + 16u * k : kDroppedOffset, 0, 0);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drec_rsrc, k < rec.y ? rbase + 16u * k : 32u * n, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
   };
   uint4* db = dbuf + 8 * it_in_wave;
-  const uint32_t L = rec.y;
   const uint32_t nb = __builtin_amdgcn_readfirstlane((maxL - 1 + 7) / 8);  // batches, wave-uniform
 #ifndef SEG_PREFETCH
 #define SEG_PREFETCH 1
@@ -371,21 +374,18 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   u16x4 blo = lo, bhi = hi;
   int32_t pb = p;
   // The 8 positions of a batch, straight-line; kAdd2 as in apply_delta.
-  auto run_batch = [&](uint32_t b, auto add2) {
+  auto run_batch = [&](auto add2) {
     constexpr bool kAdd2 = decltype(add2)::value;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const uint32_t k = 8 * b + 1 + jj;
-      uint4 d = db[jj];
-      const bool live = k < L;
-      if (!live) d = make_uint4(0u, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
+      const uint4 d = db[jj];  // past the segment's end: the sentinel record (seg_members_kernel)
       apply_delta<kAdd2>(lbase, d, blo, bhi, lo, hi);
-      const uint32_t xo = live ? (d.x & kRowMask) * (HD / 2) + col : kDroppedOffset;
+      const uint32_t xo = (d.x & kRowMask) * (HD / 2) + col;
       __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
       int32_t pc = 0;
       if constexpr (kPsqt) {
         pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta<kAdd2>(ptile, d, q));
-        const uint32_t po = (live && (int)(d.x >> 25) == q) ? (d.x & kRowMask) * 4u : kDroppedOffset;
+        const uint32_t po = (int)(d.x >> 25) == q ? (d.x & kRowMask) * 4u : kDroppedOffset;
         __builtin_amdgcn_raw_buffer_store_b32(pc, psqt_rsrc, po, 0, 0);
       }
       if constexpr (!kStar) {
@@ -401,11 +401,11 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     for (int a = 0; a + 1 < kAhead; ++a) next[a] = next[a + 1];
     next[kAhead - 1] = fetch(8 * (b + kAhead) + 1 + q);
     db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
-    // lane q of an item holds record 8b+1+q: any live one with a second add?
-    if (__ballot(8 * b + 1 + q < L && (batch.z >> 16) != kNoEntry))
-      run_batch(b, std::true_type{});
+    // lane q of an item holds record 8b+1+q: any with a second add?
+    if (__ballot((batch.z >> 16) != kNoEntry))
+      run_batch(std::true_type{});
     else
-      run_batch(b, std::false_type{});
+      run_batch(std::false_type{});
   }
 }
 
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   const __amdgpu_buffer_rsrc_t flist_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(flist), 0, kBufferAll, kBufferFlags);
   const __amdgpu_buffer_rsrc_t drec_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n), kBufferFlags);
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n + 16), kBufferFlags);
   uint2* lb = lbuf[wv];
   // Grid-stride over (unit, slice) pairs: the unit count is known only on the
   // device and its bound (seg_max_units) is far above typical counts.  The
