@@ -342,10 +342,12 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     return (live && (int)(x >> 25) == q) ? ((x & kSlotMask) * 2 + ((x >> 24) & 1)) * 4u : kDroppedOffset;
   };
   if constexpr (kPsqt) {
-    const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
+    // the list is already in registers (e): entries 2j, 2j+1 in e[j]
     uint32_t acc = (uint32_t)ptile[krow * kPsqtBuckets + q];
 #pragma unroll
-    for (int j = 0; j < 32; ++j) acc += (uint32_t)ptile[(ent[j] >> 4) * kPsqtBuckets + q];
+    for (int j = 0; j < 16; ++j)
+      acc += (uint32_t)ptile[((e[j] & 0xFFFFu) >> 4) * kPsqtBuckets + q] +
+             (uint32_t)ptile[(e[j] >> 20) * kPsqtBuckets + q];
     p = (int32_t)acc;
     __builtin_amdgcn_raw_buffer_store_b32(p, psqt_rsrc, psqt_off(rec.x, true), 0, 0);
   }
