@@ -121,7 +121,7 @@ __host__ __device__ constexpr uint32_t seg_len_bin(uint32_t L) {
 // kSegUnitPlies positions (items are sorted by length bin, a bin's items
 // counted at the bin's longest length), at most kUnitItems items.
 #ifndef SEG_UNIT_PLIES
-#define SEG_UNIT_PLIES 4096
+#define SEG_UNIT_PLIES 16384
 #endif
 constexpr uint32_t kSegUnitPlies = SEG_UNIT_PLIES;
 __host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
