@@ -71,7 +71,7 @@ SIGNATURES = {
     "fnnue_ctx_image": ([_vp, _P(_vp), _P(_sz)], _i32),
     "fnnue_ctx_free": ([_vp], None),
     "fnnue_eval_positions": ([_vp, _vp, _sz, _vp, _vp], _i32),
-    "fnnue_eval_groups": ([_vp, _vp, _vp, _sz, _i32, _vp, _vp], _i32),
+    "fnnue_eval_groups": ([_vp, _vp, _sz, _vp, _sz, _i32, _vp, _vp], _i32),
     "fnnue_eval_positions_device": ([_vp, _vp, _sz, _vp, _vp, _vp], _i32),
     "fnnue_eval_groups_device": ([_vp, _vp, _vp, _sz, _sz, _i32, _vp, _vp, _vp], _i32),
     "fnnue_ctx_check": ([_vp], _i32),
@@ -84,6 +84,7 @@ SIGNATURES = {
     "fnnue_ctx_set_timing": ([_vp, _i32], _i32),
     "fnnue_ctx_set_ft_impl": ([_vp, _i32], _i32),
     "fnnue_ctx_timing_read": ([_vp, _P(_u32), _P(C.c_double), _P(C.c_double)], _i32),
+    "fnnue_ctx_timing_phases": ([_vp, _P(_u32), _P(C.c_double), _P(C.c_double), _P(C.c_double)], _i32),
     "fnnue_build_batch_device": ([_vp, _vp, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz), _vp], _i32),
     "fnnue_build_batch": ([_vp, C.c_char_p, _sz, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_perft_device": ([_vp, C.c_char_p, _i32, _P(_u64)], _i32),

@@ -19,12 +19,14 @@
 #include "../../include/fnnue.h"
 #include "board.h"
 #include "builder.h"
+#include "internal.h"
 #include "kernels.h"
 #include "net.h"
 
 using namespace fnnue;
+using namespace fnnue::detail;
 
-namespace {
+namespace fnnue::detail {
 
 thread_local std::string g_err;
 
@@ -37,11 +39,9 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(FNNUE_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define HIP_TRY(expr, what)                    \
-  do {                                         \
-    hipError_t _e = (expr);                    \
-    if (_e != hipSuccess) return hip_fail(_e, what); \
-  } while (0)
+}  // namespace fnnue::detail
+
+namespace {
 
 // Positions per launch pair: 2^20, fewer for hd > 2047 so the transformed-
 // feature workspace (chunk * hd bytes, 1 GiB at hd = 1024) stays inside one
@@ -53,54 +53,15 @@ uint32_t chunk_for_hd(uint32_t hd) {
 
 }  // namespace
 
-struct fnnue_net {
-  Net net;
-};
-
-struct fnnue_ctx {
-  int device = 0;
-  uint32_t hd = 0;
-  uint8_t* image = nullptr;
-  size_t image_bytes = 0;
-  NetPtrs ptrs{};
-  uint32_t chunk = 0;          // positions per launch pair (chunk_for_hd)
-  uint8_t* x = nullptr;        // [chunk][hd] transformed features
-  uint8_t* bucket = nullptr;   // [chunk]
-  uint32_t* err = nullptr;     // latched position errors
-  hipStream_t stream = nullptr;
-  // host-API staging
-  fnnue_pos* d_pos = nullptr;
-  uint32_t* d_off = nullptr;
-  int32_t* d_psqt = nullptr;
-  int32_t* d_positional = nullptr;
-  size_t stage_cap = 0, off_cap = 0;
-  int ft_impl = FNNUE_FT_SLICED;
-  SlicedPlan plan{};
-  SegPlan seg{};                // incremental sliced path for groups (allocated on first use)
-  bool timing = false;
-  std::vector<std::array<hipEvent_t, 3>> evpool;  // per timed launch: before ft, between, after stack
-  size_t evused = 0;
-};
-
-namespace {
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
-};
+namespace fnnue::detail {
 
 void ctx_destroy(fnnue_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
-  for (auto& trio : c->evpool)
-    for (auto e : trio)
+  for (auto& quad : c->evpool)
+    for (auto e : quad)
       if (e) (void)hipEventDestroy(e);
+  if (c->ws_event) (void)hipEventDestroy(c->ws_event);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off,
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
@@ -163,6 +124,7 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
   if (const char* impl = std::getenv("FNNUE_FT_IMPL"))
     c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+  HIP_TRY(hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming), "hipEventCreate");
   c->ptrs = make_ptrs(c->image, hd);
   *out = c.release();
   return FNNUE_OK;
@@ -237,14 +199,18 @@ int finish_upload(fnnue_ctx* c) {
   return FNNUE_OK;
 }
 
+}  // namespace fnnue::detail
+
+namespace {
+
 // Timing events for the next launch (grown on demand, reused after a read).
-int next_events(fnnue_ctx* c, std::array<hipEvent_t, 3>** out) {
+int next_events(fnnue_ctx* c, std::array<hipEvent_t, 4>** out) {
   *out = nullptr;
   if (!c->timing) return FNNUE_OK;
   if (c->evused == c->evpool.size()) {
-    std::array<hipEvent_t, 3> trio{nullptr, nullptr, nullptr};
-    for (auto& e : trio) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
-    c->evpool.push_back(trio);
+    std::array<hipEvent_t, 4> quad{nullptr, nullptr, nullptr, nullptr};
+    for (auto& e : quad) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+    c->evpool.push_back(quad);
   }
   *out = &c->evpool[c->evused++];
   return FNNUE_OK;
@@ -265,21 +231,34 @@ int ensure_seg(fnnue_ctx* c) {
 }
 
 // Runs the stack kernel for [0, n) of the workspace and records timing.
-int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 3>* ev,
+int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 4>* ev,
                    const uint32_t* perm = nullptr, const int32_t* psqt_part = nullptr, int32_t* d_psqt = nullptr) {
-  if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
+  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s), "hipEventRecord");
   HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, perm, psqt_part, d_psqt, s),
           "stack kernel launch");
-  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s), "hipEventRecord");
+  if (ev) HIP_TRY(hipEventRecord((*ev)[3], s), "hipEventRecord");
   return FNNUE_OK;
 }
+
+// Orders this call's workspace use after the previous call's when the two
+// run on different streams (the workspace is shared by all calls on a ctx).
+int order_workspace(fnnue_ctx* c, hipStream_t s) {
+  if (c->last_stream && c->last_stream != s) {
+    HIP_TRY(hipEventRecord(c->ws_event, c->last_stream), "hipEventRecord");
+    HIP_TRY(hipStreamWaitEvent(s, c->ws_event, 0), "hipStreamWaitEvent");
+  }
+  c->last_stream = s;
+  return FNNUE_OK;
+}
+
+hipEvent_t mid_event(std::array<hipEvent_t, 4>* ev) { return ev ? (*ev)[1] : nullptr; }
 
 }  // namespace
 
 extern "C" {
 
 const char* fnnue_last_error(void) { return g_err.c_str(); }
-uint32_t fnnue_abi_version(void) { return (1u << 16) | 0u; }
+uint32_t fnnue_abi_version(void) { return (2u << 16) | 0u; }
 
 int fnnue_net_load_mem(const void* buf, size_t len, fnnue_net** out) {
   if (!buf || !out) return fail(FNNUE_E_ARG, "null argument");
@@ -431,23 +410,33 @@ int fnnue_ctx_set_timing(fnnue_ctx* ctx, int enable) {
   return FNNUE_OK;
 }
 
-int fnnue_ctx_timing_read(fnnue_ctx* ctx, uint32_t* launches, double* ft_ms, double* stack_ms) {
-  if (!ctx || !launches || !ft_ms || !stack_ms) return fail(FNNUE_E_ARG, "null argument");
+int fnnue_ctx_timing_phases(fnnue_ctx* ctx, uint32_t* launches, double* plan_ms, double* ft_ms, double* stack_ms) {
+  if (!ctx || !launches || !plan_ms || !ft_ms || !stack_ms) return fail(FNNUE_E_ARG, "null argument");
   *launches = 0;
-  *ft_ms = *stack_ms = 0;
+  *plan_ms = *ft_ms = *stack_ms = 0;
   DeviceGuard g(ctx->device);
   for (size_t i = 0; i < ctx->evused; ++i) {
     auto& e = ctx->evpool[i];
-    float a = 0, b = 0;
-    HIP_TRY(hipEventSynchronize(e[2]), "hipEventSynchronize");
+    float a = 0, b = 0, c = 0;
+    HIP_TRY(hipEventSynchronize(e[3]), "hipEventSynchronize");
     HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]), "hipEventElapsedTime");
     HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]), "hipEventElapsedTime");
-    *ft_ms += a;
-    *stack_ms += b;
+    HIP_TRY(hipEventElapsedTime(&c, e[2], e[3]), "hipEventElapsedTime");
+    *plan_ms += a;
+    *ft_ms += b;
+    *stack_ms += c;
   }
   *launches = (uint32_t)ctx->evused;
   ctx->evused = 0;
   return FNNUE_OK;
+}
+
+int fnnue_ctx_timing_read(fnnue_ctx* ctx, uint32_t* launches, double* ft_ms, double* stack_ms) {
+  if (!ctx || !launches || !ft_ms || !stack_ms) return fail(FNNUE_E_ARG, "null argument");
+  double plan = 0, ft = 0;
+  const int rc = fnnue_ctx_timing_phases(ctx, launches, &plan, &ft, stack_ms);
+  *ft_ms = plan + ft;
+  return rc;
 }
 
 int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n, int32_t* d_psqt,
@@ -457,20 +446,23 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
   if (!d_pos || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  int rc = order_workspace(ctx, s);
+  if (rc) return rc;
   for (size_t b = 0; b < n; b += ctx->chunk) {
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
-    std::array<hipEvent_t, 3>* ev = nullptr;
-    int rc = next_events(ctx, &ev);
+    std::array<hipEvent_t, 4>* ev = nullptr;
+    rc = next_events(ctx, &ev);
     if (rc) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
     const uint32_t* perm = nullptr;
     const int32_t* psqt_part = nullptr;
     if (ctx->ft_impl == FNNUE_FT_GATHER) {
+      if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
       HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_scratch launch");
     } else {
       HIP_TRY(launch_ft_sliced(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->plan, ctx->x, d_psqt + b, ctx->bucket,
-                               ctx->err, s),
+                               ctx->err, s, mid_event(ev)),
               "ft_sliced launch");
       perm = ctx->plan.perm;
       psqt_part = ctx->plan.psqt_part;
@@ -491,18 +483,19 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
   if (!d_pos || !d_off || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  if (int rc = order_workspace(ctx, s)) return rc;
   if (ctx->ft_impl == FNNUE_FT_SLICED) {
     int rc = ensure_seg(ctx);
     if (rc) return rc;
     if (npos <= ctx->chunk) {
       // One launch: the offsets never come to the host (no D2H round trip and
       // no stream drain per call); they are checked on the device instead.
-      std::array<hipEvent_t, 3>* ev = nullptr;
+      std::array<hipEvent_t, 4>* ev = nullptr;
       if ((rc = next_events(ctx, &ev))) return rc;
       if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
       HIP_TRY(launch_groups_check(d_off, (uint32_t)ngroups, (uint32_t)npos, ctx->err, s), "offset check launch");
       HIP_TRY(launch_ft_segments(ctx->hd, d_pos, (uint32_t)npos, d_off, (uint32_t)ngroups, 0, mode, ctx->ptrs,
-                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s),
+                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
               "ft_segments launch");
       return run_chunk_tail(ctx, (uint32_t)npos, d_positional, s, ev, nullptr, ctx->plan.psqt_part, d_psqt);
     }
@@ -520,16 +513,17 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
     }
     if (ge == gb) return fail(FNNUE_E_ARG, "a group is larger than the device workspace");
     const uint32_t base = off[gb], m = off[ge] - off[gb];
-    std::array<hipEvent_t, 3>* ev = nullptr;
+    std::array<hipEvent_t, 4>* ev = nullptr;
     int rc = next_events(ctx, &ev);
     if (rc) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
     if (ctx->ft_impl == FNNUE_FT_SLICED) {
       HIP_TRY(launch_ft_segments(ctx->hd, d_pos + base, m, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs,
-                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s),
+                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
               "ft_segments launch");
       rc = run_chunk_tail(ctx, m, d_positional + base, s, ev, nullptr, ctx->plan.psqt_part, d_psqt + base);
     } else {
+      if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
       HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs, ctx->x,
                                d_psqt + base, ctx->bucket, ctx->err, s),
               "ft_groups launch");
@@ -572,16 +566,17 @@ int fnnue_eval_positions(fnnue_ctx* ctx, const fnnue_pos* pos, size_t n, int32_t
   return FNNUE_OK;
 }
 
-int fnnue_eval_groups(fnnue_ctx* ctx, const fnnue_pos* pos, const uint32_t* off, size_t ngroups, int mode,
-                      int32_t* psqt, int32_t* positional) {
+int fnnue_eval_groups(fnnue_ctx* ctx, const fnnue_pos* pos, size_t npos, const uint32_t* off, size_t ngroups,
+                      int mode, int32_t* psqt, int32_t* positional) {
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
   if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
-  if (ngroups == 0) return FNNUE_OK;
+  if (ngroups == 0) return npos == 0 ? FNNUE_OK : fail(FNNUE_E_ARG, "positions without groups");
+  if (ngroups > 0xFFFFFFFFu || npos > 0xFFFFFFFFu) return fail(FNNUE_E_ARG, "batch too large");
   if (!pos || !off || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
   if (off[0] != 0) return fail(FNNUE_E_ARG, "off[0] must be 0");
   for (size_t g = 0; g < ngroups; ++g)
     if (off[g + 1] < off[g]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
-  const size_t npos = off[ngroups];
+  if (off[ngroups] != npos) return fail(FNNUE_E_ARG, "off[ngroups] must equal npos");
   DeviceGuard g(ctx->device);
   int rc = ensure_stage(ctx, std::max<size_t>(npos, 1), ngroups + 1);
   if (rc) return rc;

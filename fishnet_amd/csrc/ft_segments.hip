@@ -26,8 +26,9 @@
 //   seg_members   delta records placed at root + rank (a segment's plies
 //                 contiguous)
 //   seg_count / plan_scan / seg_scatter   counting sort of items by
-//                 (king block, length bin), unit table cut at ~4096
-//                 positions, full lists (write_rows)
+//                 (king block, length bin), unit table cut every
+//                 kSegUnitPlies (16384) positions of work per king block,
+//                 full lists (write_rows)
 //   ft_segments   (unit, slice) workgroups, XCD-aware, tile in LDS
 // then stack_kernel over x / bucket / psqt_part in position order.
 #include <hip/hip_runtime.h>
@@ -434,9 +435,11 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
   constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
   // Buffer ranges are this launch's exact extents (x: n rows of HD bytes,
-  // < 2^31; psqt_part: 2n words; drec: 2n records): finished items store and
-  // load at kDroppedOffset, past num_records, so the hardware drops them, and
-  // no record can reach beyond the launch's rows.
+  // < 2^31; psqt_part: 2n words; drec: 2n + 1 records, the last the sentinel
+  // record 2n).  Items past their segment's end read the sentinel, whose x row
+  // 2n and PSQT word 2n fall just past the x and psqt_part ranges, so the
+  // hardware drops those stores; other dropped stores use kDroppedOffset.  No
+  // record can reach beyond the launch's rows.
   const __amdgpu_buffer_rsrc_t psqt_rsrc = __builtin_amdgcn_make_buffer_rsrc(psqt_part, 0, (int)(8 * n), kBufferFlags);
   const __amdgpu_buffer_rsrc_t x_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(x, 0, (int)min((uint64_t)n * HD, (uint64_t)kBufferRange), kBufferFlags);
@@ -559,7 +562,7 @@ hipError_t launch_groups_check(const uint32_t* off, uint32_t ngroups, uint32_t n
 
 hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
                               uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
-                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid) {
   if (n == 0) return hipSuccess;
   const bool star = mode == FNNUE_GROUP_STAR;
   hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
@@ -594,6 +597,7 @@ hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, con
   hipLaunchKernelGGL(seg_scatter_kernel, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.cref, G.ipos,
                      G.len, P.ctr, (uint4*)G.items, P.flist);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
   const uint32_t mu = seg_max_units(n);
 #define CALL(H) ft_segments_t<H>(G, P, net, n, star, x, mu, stream)
   FNNUE_HD_DISPATCH(hd, CALL)

@@ -339,8 +339,10 @@ hipError_t launch_sliced_ft(uint32_t hd, uint32_t n, const NetPtrs& net, const S
 }
 
 hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
-                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
-  const hipError_t e = launch_sliced_plan(pos, n, P, psqt, bucket, err, stream);
+                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream,
+                            hipEvent_t mid) {
+  hipError_t e = launch_sliced_plan(pos, n, P, psqt, bucket, err, stream);
+  if (e == hipSuccess && mid) e = hipEventRecord(mid, stream);
   return e != hipSuccess ? e : launch_sliced_ft(hd, n, net, P, x, stream);
 }
 

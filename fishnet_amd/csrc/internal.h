@@ -1,0 +1,85 @@
+// internal.h — host-side internals shared by the C ABI translation units
+// (capi.cpp: single-device contexts; multi.cpp: one process driving several
+// devices over RCCL).  Not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <string>
+#include <vector>
+
+#include "../../include/fnnue.h"
+#include "kernels.h"
+#include "net.h"
+
+struct fnnue_net {
+  fnnue::Net net;
+};
+
+struct fnnue_ctx {
+  int device = 0;
+  uint32_t hd = 0;
+  uint8_t* image = nullptr;
+  size_t image_bytes = 0;
+  fnnue::NetPtrs ptrs{};
+  uint32_t chunk = 0;          // positions per launch pair (chunk_for_hd)
+  uint8_t* x = nullptr;        // [chunk][hd] transformed features
+  uint8_t* bucket = nullptr;   // [chunk]
+  uint32_t* err = nullptr;     // latched position errors
+  hipStream_t stream = nullptr;
+  // host-API staging
+  fnnue_pos* d_pos = nullptr;
+  uint32_t* d_off = nullptr;
+  int32_t* d_psqt = nullptr;
+  int32_t* d_positional = nullptr;
+  size_t stage_cap = 0, off_cap = 0;
+  int ft_impl = FNNUE_FT_SLICED;
+  fnnue::SlicedPlan plan{};
+  fnnue::SegPlan seg{};                // incremental sliced path for groups (allocated on first use)
+  bool timing = false;
+  // per timed launch: before the FT plan, before the FT main kernel, before the
+  // layer stacks, after them
+  std::vector<std::array<hipEvent_t, 4>> evpool;
+  size_t evused = 0;
+  // Workspace ordering across streams: every *_device call writes the same
+  // workspace (x, bucket, plan, err); a call on a different stream than the
+  // previous one first waits for the previous one's work (ws_event).
+  hipStream_t last_stream = nullptr;
+  hipEvent_t ws_event = nullptr;
+};
+
+
+namespace fnnue::detail {
+
+extern thread_local std::string g_err;
+int fail(int code, const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+
+#define HIP_TRY(expr, what)                              \
+  do {                                                   \
+    hipError_t _e = (expr);                              \
+    if (_e != hipSuccess) return ::fnnue::detail::hip_fail(_e, what); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+void ctx_destroy(fnnue_ctx* c);
+// Allocates a context on `device` for width hd: everything except the image contents.
+int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out);
+// Derives the LDS-tile layout of the FT weights from the (just written) image.
+int finish_upload(fnnue_ctx* c);
+// Reads and clears the latched device error word.
+int latched(fnnue_ctx* c);
+// After FNNUE_E_POSITION latched: names the first invalid position.
+int name_invalid(int rc, const fnnue_pos* pos, size_t n);
+
+}  // namespace fnnue::detail

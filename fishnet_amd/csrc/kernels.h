@@ -64,8 +64,10 @@ hipError_t launch_sliced_plan(const fnnue_pos* pos, uint32_t n, const SlicedPlan
 hipError_t launch_sliced_ft(uint32_t hd, uint32_t n, const NetPtrs& net, const SlicedPlan& P, uint8_t* x,
                             hipStream_t stream);
 // Writes psqt[pos], x[slot], bucket[slot] and P.perm; then run launch_stack with P.perm.
+// `mid` (optional) is recorded between the plan and the main kernel (phase timing).
 hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,
-                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream);
+                            uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream,
+                            hipEvent_t mid = nullptr);
 
 // Incremental FT on LDS tiles for CHAIN / STAR groups (ft_segments.hip).
 // Uses the sliced plan's tiles, counters, unit table, lists and psqt_part;
@@ -87,7 +89,8 @@ size_t seg_scan_temp_bytes(uint32_t chunk);
 uint32_t seg_max_units(uint32_t chunk);  // unit-table entries ft_segments may need
 hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
                               uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
-                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream);
+                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream,
+                              hipEvent_t mid = nullptr);
 
 // Device-side check of group offsets (non-decreasing, spanning [0, npos)):
 // latches error bit 2 (FNNUE_E_ARG).  ft_segments stays in bounds regardless.

@@ -117,10 +117,14 @@ class Evaluator:
     def eval_groups(self, pos: np.ndarray, off: np.ndarray, mode: int = N.GROUP_CHAIN):
         pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
         off = np.ascontiguousarray(off, dtype=np.uint32)
-        n = int(off[-1]) if len(off) else 0
+        if len(off) < 1:
+            raise ValueError("off needs at least one entry (off[0] = 0)")
+        n = pos.shape[0]
+        if int(off[-1]) != n:
+            raise ValueError(f"off[-1] = {int(off[-1])} but {n} positions were given")
         psqt = np.zeros(n, dtype=np.int32)
         positional = np.zeros(n, dtype=np.int32)
-        N.check(N.lib.fnnue_eval_groups(self._h, N.ptr(pos), N.ptr(off), len(off) - 1, mode,
+        N.check(N.lib.fnnue_eval_groups(self._h, N.ptr(pos), n, N.ptr(off), len(off) - 1, mode,
                                         N.ptr(psqt), N.ptr(positional)))
         return psqt, positional
 
@@ -163,6 +167,12 @@ class Evaluator:
 
     def set_timing(self, enable: bool) -> None:
         N.check(N.lib.fnnue_ctx_set_timing(self._h, 1 if enable else 0))
+
+    def timing_phases(self) -> tuple[int, float, float, float]:
+        """(timed launches, summed ms of the FT plan kernels, of the FT main kernel, of the layer stacks); resets."""
+        n, a, b, c = C.c_uint32(), C.c_double(), C.c_double(), C.c_double()
+        N.check(N.lib.fnnue_ctx_timing_phases(self._h, C.byref(n), C.byref(a), C.byref(b), C.byref(c)))
+        return n.value, a.value, b.value, c.value
 
     def timing_read(self) -> tuple[int, float, float]:
         """(timed launches, summed feature-transformer ms, summed layer-stack ms); resets."""

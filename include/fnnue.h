@@ -18,8 +18,11 @@
  *    the library.  *_device entry points take device pointers and a hipStream_t
  *    (as void*), enqueue work and return without synchronising.
  *  - A fnnue_net is immutable and may be shared across threads; a fnnue_ctx
- *    must not be used from two threads at once (one ctx per GPU, one process
- *    per GPU — the analogue of one engine per worker, [ref] src/main.rs:158-170).
+ *    must not be used from two threads at once (one ctx per GPU — the analogue
+ *    of one engine per worker, [ref] src/main.rs:158-170).  Calls on one ctx
+ *    share its device workspace: *_device calls on different streams are
+ *    ordered by the library (a call on a new stream waits for the previous
+ *    call's stream), so they serialise rather than race.
  *  - Outputs per position are the two raw Stockfish NNUE terms, before
  *    optimism / material scaling (upstream evaluate_nnue.cpp evaluate()):
  *      psqt       = (psqtAcc[stm][bucket] - psqtAcc[~stm][bucket]) / 2
@@ -102,6 +105,40 @@ int fnnue_ctx_create_from_image(int device, uint32_t hd, const void *device_imag
 int fnnue_ctx_image(fnnue_ctx *ctx, const void **device_image, size_t *bytes);
 void fnnue_ctx_free(fnnue_ctx *ctx);
 
+/* ---- several GPUs from one process ----
+ * The reference runs one engine per core ([ref] src/main.rs:156-170,
+ * src/configure.rs:196-206: Cores::All = available_parallelism).  A
+ * fnnue_multi owns one context per listed device: the net is uploaded once to
+ * devices[0] and RCCL-broadcast over xGMI (ncclCommInitAll, one communicator
+ * per device, this process); batches are sharded with no data-path
+ * collective — contiguous position ranges, or whole groups balanced by
+ * position count (fnnue_partition_groups) — and each device's results land in
+ * its disjoint slice of the caller's buffers.  Same results as one context. */
+typedef struct fnnue_multi fnnue_multi;
+int fnnue_multi_create(const fnnue_net *net, const int *devices, int ndev, fnnue_multi **out);
+void fnnue_multi_free(fnnue_multi *m);
+int fnnue_multi_size(const fnnue_multi *m, int *ndev);
+/* The context of device i (borrowed; owned by m). */
+int fnnue_multi_ctx(fnnue_multi *m, int i, fnnue_ctx **ctx);
+/* Host buffers, synchronous: one host thread per device (H2D, eval, D2H). */
+int fnnue_multi_eval_positions(fnnue_multi *m, const fnnue_pos *pos, size_t n, int32_t *psqt, int32_t *positional);
+int fnnue_multi_eval_groups(fnnue_multi *m, const fnnue_pos *pos, size_t npos, const uint32_t *off, size_t ngroups,
+                            int mode, int32_t *psqt, int32_t *positional);
+/* Device buffers: arrays of one pointer / count per device (device i's
+ * buffers live on device i); enqueued on each context's own stream, returns
+ * without synchronising.  fnnue_multi_sync drains every device and reports
+ * latched errors (as fnnue_ctx_check). */
+int fnnue_multi_eval_positions_device(fnnue_multi *m, const fnnue_pos *const *d_pos, const size_t *n,
+                                      int32_t *const *d_psqt, int32_t *const *d_positional);
+int fnnue_multi_eval_groups_device(fnnue_multi *m, const fnnue_pos *const *d_pos, const uint32_t *const *d_off,
+                                   const size_t *ngroups, const size_t *npos, int mode, int32_t *const *d_psqt,
+                                   int32_t *const *d_positional);
+int fnnue_multi_sync(fnnue_multi *m);
+/* Splits groups off[0..ngroups] into nparts contiguous runs of whole groups
+ * with about equal position counts: part k = groups [cut[k], cut[k+1]),
+ * cut has nparts + 1 entries.  Host only. */
+int fnnue_partition_groups(const uint32_t *off, size_t ngroups, int nparts, uint32_t *cut);
+
 /* ---- evaluation, host buffers (synchronous) ----
  * Copies in, runs the device path, copies out.  Position validity is checked
  * on the device; an invalid position fails the whole call with
@@ -121,8 +158,11 @@ int fnnue_eval_positions(fnnue_ctx *ctx, const fnnue_pos *pos, size_t n, int32_t
  * Results are identical to fnnue_eval_positions on the same positions. */
 #define FNNUE_GROUP_CHAIN 0
 #define FNNUE_GROUP_STAR 1
-int fnnue_eval_groups(fnnue_ctx *ctx, const fnnue_pos *pos, const uint32_t *off, size_t ngroups, int mode,
-                      int32_t *psqt, int32_t *positional);
+/* pos holds npos positions; off has ngroups + 1 entries, off[0] = 0,
+ * non-decreasing, off[ngroups] = npos (else FNNUE_E_ARG, nothing read past
+ * pos[npos - 1]). */
+int fnnue_eval_groups(fnnue_ctx *ctx, const fnnue_pos *pos, size_t npos, const uint32_t *off, size_t ngroups,
+                      int mode, int32_t *psqt, int32_t *positional);
 
 /* ---- evaluation, device buffers (asynchronous on `stream`, a hipStream_t) ----
  * Inputs already resident in HBM; results written to device memory.  Position
@@ -220,6 +260,9 @@ int fnnue_ctx_set_ft_impl(fnnue_ctx *ctx, int impl);
  * summed kernel times (ms), and resets the accumulators. */
 int fnnue_ctx_set_timing(fnnue_ctx *ctx, int enable);
 int fnnue_ctx_timing_read(fnnue_ctx *ctx, uint32_t *launches, double *ft_ms, double *stack_ms);
+/* Same, split into the FT plan kernels, the FT main kernel (ft_slices /
+ * ft_segments / ft_scratch / ft_groups) and the layer stacks. */
+int fnnue_ctx_timing_phases(fnnue_ctx *ctx, uint32_t *launches, double *plan_ms, double *ft_ms, double *stack_ms);
 
 #ifdef __cplusplus
 }

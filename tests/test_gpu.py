@@ -333,3 +333,63 @@ def test_device_groups_offsets_checked_on_device(ev_cache):
                               stream)
         ev.check()
         assert np.array_equal(ps.cpu().numpy(), ops) and np.array_equal(po.cpu().numpy(), opo)
+
+
+def test_segments_units_split_inside_king_block(ev_cache):
+    """Many segments in ONE king block (the kings' start squares): far more than
+    2 x kSegUnitPlies (16384) plies of work there, so plan_scan cuts the king
+    block's length bins into several units mid-bin (sliced_common.h
+    build_units).  CHAIN over 5000 random games and STAR over the children of
+    150 games, both against the oracle."""
+    ev, on = ev_cache()
+    for mode, pm, count in ((N.GROUP_CHAIN, N.PLAYOUT_PLIES, 5000), (N.GROUP_STAR, N.PLAYOUT_CHILDREN, 150)):
+        pos, off = F.random_playouts(77, count, mode=pm, threads=8)
+        board = np.zeros((len(pos), 64), np.uint8)
+        board[:, 0::2] = pos[:, :32] & 15
+        board[:, 1::2] = pos[:, :32] >> 4
+        assert int((board[:, 4] == 6).sum()) > 2 * 16384  # white king on e1: one king block
+        ps, po = ev.eval_groups(pos, off, mode)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert rc == 0
+        assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
+def test_eval_groups_rejects_bad_offsets(ev_cache):
+    """Host API: offsets must end at the number of positions given (no read past
+    the input) and there must be at least one offset."""
+    ev, _ = ev_cache()
+    pos, off = F.random_playouts(3, 5, mode=N.PLAYOUT_PLIES, threads=2)
+    bad = off.copy()
+    bad[-1] += 1
+    with pytest.raises(ValueError):
+        ev.eval_groups(pos, bad, N.GROUP_CHAIN)
+    with pytest.raises(ValueError):
+        ev.eval_groups(pos, np.zeros(0, np.uint32), N.GROUP_CHAIN)
+    import ctypes as C
+    ps = np.zeros(len(pos), np.int32)
+    po = np.zeros(len(pos), np.int32)
+    rc = N.lib.fnnue_eval_groups(ev.handle, N.ptr(pos), len(pos) - 1, N.ptr(off), len(off) - 1, N.GROUP_CHAIN,
+                                 N.ptr(ps), N.ptr(po))
+    assert rc == -1 and b"npos" in N.lib.fnnue_last_error()
+
+
+def test_device_calls_on_two_streams(ev_cache):
+    """Two *_device calls on different streams with no sync in between: the
+    library orders the shared workspace, both results exact."""
+    import torch
+    ev, on = ev_cache()
+    a = F.random_playouts(41, 200_000, threads=8)
+    b = F.random_playouts(42, 200_000, threads=8)
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    da, db = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    out = [torch.zeros(len(a), dtype=torch.int32, device=dev) for _ in range(4)]
+    torch.cuda.synchronize()
+    ev.eval_positions_device(da.data_ptr(), len(a), out[0].data_ptr(), out[1].data_ptr(), s1.cuda_stream)
+    ev.eval_positions_device(db.data_ptr(), len(b), out[2].data_ptr(), out[3].data_ptr(), s2.cuda_stream)
+    torch.cuda.synchronize()
+    ev.check()
+    for pos, ps, po in ((a, out[0], out[1]), (b, out[2], out[3])):
+        idx = np.arange(0, len(pos), 13)
+        ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+        assert np.array_equal(ps.cpu().numpy()[idx], ops) and np.array_equal(po.cpu().numpy()[idx], opo)

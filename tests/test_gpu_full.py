@@ -1,13 +1,20 @@
-"""Full-size parity run (north star: "bit-exact NNUE evals for >= 1e8 positions
-per run"): BASELINE config 4's workload — every ply of random games plus all
-their legal 1-ply children, >= 1e8 positions — evaluated on one MI355X by both
-device paths (incremental STAR groups and from-scratch sliced), and EVERY
-result compared with the CPU oracle.
+"""Full-size parity runs, on by default in `-m gpu`.
 
-Opt-in (it takes about a minute of host time): FNNUE_FULL=<positions> on the
-GPU box, e.g.
-    FNNUE_FULL=100000000 python -u -m pytest tests/test_gpu_full.py -m gpu -s
-A JSON record goes to gpurun_out/full_parity.json.
+* test_full_size_parity — north star "bit-exact NNUE evals for >= 1e8
+  positions per run": BASELINE config 4's workload (every ply of random games
+  plus all their legal 1-ply children, >= 1e8 positions) evaluated on one
+  MI355X by both device paths (incremental STAR groups and from-scratch
+  sliced), and EVERY result compared with the CPU oracle.  The expansion
+  mirrors [ref] src/queue.rs:571-606 (every ply of every game) plus the
+  children of SURVEY.md §8d config 4.
+* test_config3_full_size — BASELINE config 3 at its full size: 10,000
+  random-playout games (seed 2), every ply through the incremental CHAIN
+  path with the big (HD 1024) and the small (HD 128) net, every ply of both
+  compared with the oracle.
+
+FNNUE_FULL=<positions> overrides the config-4 size (default 1e8).  JSON
+records go to gpurun_out/full_parity.json and gpurun_out/config3_full.json.
+Host cost on the GPU box (16 threads): ~10 s generation, ~20 s oracle.
 """
 import json
 import os
@@ -22,14 +29,28 @@ from tests.conftest import ROOT, net_bytes
 
 pytestmark = pytest.mark.gpu
 
-TARGET = int(os.environ.get("FNNUE_FULL", "0"))
+TARGET = int(os.environ.get("FNNUE_FULL", "100000000"))
 
 
-@pytest.mark.skipif(TARGET <= 0, reason="opt-in: set FNNUE_FULL=<positions>")
+def _threads() -> int:
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:
+        return max(1, min(16, os.cpu_count() or 1))
+
+
+def _record(name: str, rec: dict) -> None:
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", name), "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec), flush=True)
+
+
+@pytest.mark.timeout(900)
 def test_full_size_parity():
     import torch
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = _threads()
     t0 = time.time()
     pos_parts, off_parts, total, seed, base = [], [np.zeros(1, np.int64)], 0, 3, 0
     while total < TARGET:  # config 4: seed 3, games of U[0,160] plies + all legal children
@@ -82,7 +103,7 @@ def test_full_size_parity():
     on = OracleNet(data)
     mism = 0
     t = time.perf_counter()
-    step = 5_000_000
+    step = 10_000_000
     for lo in range(0, n, step):
         hi = min(n, lo + step)
         ops, opo, rc = on.eval_packed(pos[lo:hi], threads=threads)
@@ -91,16 +112,42 @@ def test_full_size_parity():
         print(f"oracle {hi}/{n} mismatches so far {mism} ({time.perf_counter() - t:.0f} s)", flush=True)
     t_oracle = time.perf_counter() - t
 
-    rec = {"workload": "BASELINE config 4: random games (seed 3, L~U[0,160]) + all legal 1-ply children, "
-                       "synthetic SFNNv5 net HD 1024",
-           "positions": n, "groups": ng, "gen_s": round(t_gen, 1),
-           "gpu_s": {k: round(v, 3) for k, v in times.items()},
-           "gpu_positions_per_s": {k: round(n / v) for k, v in times.items()},
-           "oracle_s": round(t_oracle, 1), "oracle_threads": threads,
-           "mismatches_vs_oracle": mism, "groups_vs_positions_mismatches": paths_agree}
-    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "full_parity.json"), "w") as f:
-        json.dump(rec, f, indent=1)
-    print(json.dumps(rec), flush=True)
+    _record("full_parity.json", {
+        "test": "tests/test_gpu_full.py::test_full_size_parity",
+        "workload": "BASELINE config 4: random games (seed 3, L~U[0,160]) + all legal 1-ply children, "
+                    "synthetic SFNNv5 net HD 1024",
+        "positions": n, "groups": ng, "gen_s": round(t_gen, 1),
+        "gpu_s": {k: round(v, 3) for k, v in times.items()},
+        "gpu_positions_per_s": {k: round(n / v) for k, v in times.items()},
+        "oracle_s": round(t_oracle, 1), "oracle_threads": threads,
+        "mismatches_vs_oracle": mism, "groups_vs_positions_mismatches": paths_agree})
     assert paths_agree == 0
     assert mism == 0
+
+
+@pytest.mark.timeout(600)
+def test_config3_full_size():
+    """10k random games (seed 2, L~U[0,160]), every ply, big HD-1024 + small HD-128 net, CHAIN."""
+    threads = _threads()
+    pos, off = F.random_playouts(2, 10_000, 0, 160, mode=F.PLAYOUT_PLIES, threads=threads)
+    n, ng = len(pos), len(off) - 1
+    rec = {"test": "tests/test_gpu_full.py::test_config3_full_size",
+           "workload": "BASELINE config 3: 10,000 random-playout games (seed 2, L~U[0,160]), every ply, "
+                       "incremental CHAIN; big (HD 1024) + small (HD 128) synthetic nets",
+           "positions": n, "games": ng, "nets": {}}
+    bad = 0
+    for hd, seed in ((1024, 1), (128, 1001)):
+        data = net_bytes(seed, hd, 0)
+        ev = F.Evaluator(F.Net.from_bytes(data), 0)
+        t = time.perf_counter()
+        ps, po = ev.eval_groups(pos, off, F.GROUP_CHAIN)
+        t_gpu = time.perf_counter() - t
+        ev.close()
+        ops, opo, rc = OracleNet(data).eval_packed(pos, threads=threads)
+        assert rc == 0
+        m = int(((ps != ops) | (po != opo)).sum())
+        bad += m
+        rec["nets"][f"hd{hd}"] = {"mismatches_vs_oracle": m, "gpu_host_api_s": round(t_gpu, 3)}
+    _record("config3_full.json", rec)
+    assert n > 700_000
+    assert bad == 0

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert N.lib.fnnue_abi_version() >> 16 == 1
+    assert N.lib.fnnue_abi_version() >> 16 == 2  # 2.0: fnnue_eval_groups takes npos
 
 
 def test_net_parse_and_info():
