@@ -7,22 +7,34 @@ Default workload (N=1 headline) = BASELINE config 2 (configs[1]): 1,000,000
 random-playout positions per GPU (splitmix64 seed 1, L ~ U[0,160] random legal
 plies), synthetic SFNNv5 net with HD = 1024 (same shapes and file format as
 nn-ad9b42354671.nnue, which is not available offline), accumulators from
-scratch.  A step = one fnnue_eval_*_device call over the HBM-resident batch.
-For N > 1 every rank evaluates its own shard (weak scaling; positions are
-independent, no data-path collective); the net image is RCCL-broadcast from
-rank 0 once at start-up.
+scratch.  A step = one evaluation call over the HBM-resident batch of every
+GPU.  Weak scaling: every GPU evaluates its own 1M-position shard; positions
+are independent, so there is no data-path collective.
 
-Other workloads (not the headline line; the other BASELINE configs, measured for DESIGN.md):
+N > 1, two launch forms, both measuring N GPUs (n_gpus = N is asserted):
+  * torchrun --nproc-per-node N bench.py --gpus N   one process per GPU; the
+    net image is RCCL-broadcast from rank 0 (torch.distributed "nccl"); the
+    timed region is closed by a barrier, the max over ranks is taken; results
+    are then gathered to rank 0 over RCCL (gather_ms, outside `value`).
+  * python bench.py --gpus N                         one process driving N
+    GPUs through the C ABI's fnnue_multi (ncclCommInitAll + ncclBroadcast of
+    the image inside libfnnue.so, one stream per device).
+
+Other workloads (the other BASELINE configs, measured for DESIGN.md):
   --workload games     config 3: random-playout games, every ply, incremental (CHAIN)
   --workload children  config 4: every ply of random games plus all legal children (STAR)
   --small-net 128      also evaluate every position with a small net each step (config 3's big + small)
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
+roofline: the binding resource of the dominant kernel (ft_slices for config
+2, ft_segments for configs 3/4) from the committed PMC profile of this tree
+(profiles/counters.json, tools/profile_round.sh + tools/roofline.py): VALU
+issue, LDS-array busy and bytes past L2, each over the kernel's live time
+measured here with HIP events on its launch stream; `frac` = the largest.
 """
 from __future__ import annotations
 
 import argparse
+import importlib.util
 import json
 import os
 import sys
@@ -34,9 +46,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
-VALU_PEAK = 256 * 4 * 2.4e9 / 4  # VOP3-class wave64 instructions/s: 1024 SIMDs, 4 cycles each at 2.4 GHz
+CLOCK_HZ = 2.4e9  # spec peak engine clock
+CUS, SIMDS = 256, 1024
+VALU_PEAK = SIMDS * CLOCK_HZ / 4  # 64-bit-encoded wave64 VALU instructions/s (4 cycles each per SIMD)
+LDS_PEAK = CUS * CLOCK_HZ  # LDS-array busy cycles/s over all CUs
 METRIC = "NNUE positions evaluated/sec (1–8 MI355X) + % HBM roofline, bit-exact"
 PSQT_BUCKETS = 8
+MAIN_KERNEL = {("positions", "sliced"): "ft_slices_kernel", ("positions", "gather"): "ft_scratch_kernel",
+               ("groups", "sliced"): "ft_segments_kernel", ("groups", "gather"): "ft_groups_kernel"}
 
 
 def parse_args():
@@ -55,10 +72,46 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true", help="skip timing the host-buffer entry points")
-    ap.add_argument("--threads", type=int, default=0, help="host threads (0 = min(16, cpu_count))")
+    ap.add_argument("--threads", type=int, default=0, help="host threads (0 = every core this process may use)")
     ap.add_argument("--ft-impl", choices=["sliced", "gather"], default="sliced",
                     help="feature-transformer kernel for independent positions")
+    ap.add_argument("--launch", choices=["auto", "devices"], default="auto",
+                    help="devices: drive the GPUs through fnnue_multi from this process even at --gpus 1 "
+                         "(auto: torchrun ranks if WORLD_SIZE > 1, else fnnue_multi for --gpus > 1)")
     return ap.parse_args()
+
+
+def host_cpus() -> dict:
+    """The host cores this process may use ([ref] src/configure.rs:196-206:
+    Cores::All = available_parallelism, i.e. the affinity set / cgroup quota)."""
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = total
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota + 0.999)))
+    share = os.environ.get("OMP_NUM_THREADS")
+    # The GPU box exports OMP_NUM_THREADS = its CPU share per GPU (16); a box
+    # whose affinity set shows the whole machine is capped to that share.
+    if share and share.isdigit() and 0 < int(share) < usable:
+        usable = int(share)
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "os_cpu_count": total, "affinity": aff, "cgroup_quota": quota,
+            "omp_num_threads": share, "model": model}
 
 
 def boards_of(pos: np.ndarray) -> np.ndarray:
@@ -88,6 +141,54 @@ def rows_incremental(board: np.ndarray, base: np.ndarray, has_base: np.ndarray) 
     return rows
 
 
+def tree_hash() -> str:
+    spec = importlib.util.spec_from_file_location("roofline_tool", os.path.join(ROOT, "tools", "roofline.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.tree_hash()
+
+
+def resource_fractions(c: dict, t_s: float) -> dict:
+    """Fractions of VALU issue, LDS-array busy and HBM for one launch of a
+    kernel whose per-launch counters are `c`, running t_s seconds."""
+    fr = {}
+    if c.get("SQ_INSTS_VALU"):
+        fr["valu"] = {"achieved": c["SQ_INSTS_VALU"] / t_s, "peak": VALU_PEAK, "unit": "VALU wave-instr/s"}
+    if c.get("SQ_LDS_IDX_ACTIVE"):
+        fr["lds"] = {"achieved": c["SQ_LDS_IDX_ACTIVE"] / t_s, "peak": LDS_PEAK, "unit": "LDS-busy CU-cycles/s"}
+    if c.get("FETCH_SIZE") is not None and c.get("WRITE_SIZE") is not None:
+        b = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        fr["hbm"] = {"achieved": b / t_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "bytes": b}
+    for v in fr.values():
+        v["frac"] = round(v["achieved"] / v["peak"], 4)
+        v["achieved"] = round(v["achieved"], 1) if v["unit"] == "GB/s" else float(f"{v['achieved']:.4g}")
+    return fr
+
+
+class Shard:
+    """One GPU's HBM-resident inputs and outputs."""
+
+    def __init__(self, torch, dev, pos, off, small):
+        self.dev = dev
+        self.n = len(pos)
+        self.pos = torch.from_numpy(pos).to(dev)
+        self.off = torch.from_numpy(off.astype(np.uint32).view(np.int32)).to(dev) if off is not None else None
+        self.ng = len(off) - 1 if off is not None else 0
+        self.psqt = torch.zeros(self.n, dtype=torch.int32, device=dev)
+        self.positional = torch.zeros(self.n, dtype=torch.int32, device=dev)
+        self.small = torch.zeros(2, self.n, dtype=torch.int32, device=dev) if small else None
+
+
+def make_inputs(F, args, seed, threads):
+    off = None
+    if args.workload == "positions":
+        pos = F.random_playouts(seed, args.positions, 0, 160, threads=threads)
+    else:
+        mode = F.PLAYOUT_PLIES if args.workload == "games" else F.PLAYOUT_CHILDREN
+        pos, off = F.random_playouts(seed + 1, args.games, 0, 160, mode=mode, threads=threads)
+    return pos, off
+
+
 def main():
     args = parse_args()
     import torch
@@ -97,55 +198,70 @@ def main():
     from fishnet_amd import dist as D
 
     rank, world, local = D.env_rank()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    threads = args.threads or min(16, os.cpu_count() or 1)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    dist_on = world > 1
+    if world > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch N ranks for N GPUs")
+    launch = "ranks" if world > 1 else ("devices" if args.gpus > 1 or args.launch == "devices" else "single")
+    ndev_here = args.gpus if launch == "devices" else 1
+    have = F.device_count()
+    need = (local + 1) if launch != "devices" else args.gpus
+    if have < need:
+        raise SystemExit(f"bench needs {need} visible GPU(s) for --gpus {args.gpus}, found {have}")
+    devices = list(range(args.gpus)) if launch == "devices" else [local]
+    cpus = host_cpus()
+    threads = args.threads or cpus["usable"]
+    torch.cuda.set_device(devices[0])
+    dist_on = launch == "ranks"
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    groups = args.workload != "positions"
+    gmode = None if not groups else (F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR)
 
-    # ---- net: synthesized on rank 0, device image broadcast over RCCL/xGMI ----
+    # ---- net: rank 0 / device 0 holds it, RCCL broadcasts it over xGMI ----
     t0 = time.time()
-    image = F.Net.from_bytes(F.synthesize_net(args.seed, args.hd, 0)).image() if rank == 0 else None
-    img = D.broadcast_image(image, dev) if dist_on else torch.from_numpy(image).to(dev)
-    torch.cuda.synchronize()
-    ev = F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=args.hd)
-    ev.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
-    del img
-    ev_small = None
-    if args.small_net:
-        image2 = (F.Net.from_bytes(F.synthesize_net(args.seed + 1000, args.small_net, 0)).image()
-                  if rank == 0 else None)
-        img2 = D.broadcast_image(image2, dev) if dist_on else torch.from_numpy(image2).to(dev)
-        torch.cuda.synchronize()
-        ev_small = F.Evaluator(None, local, image_ptr=img2.data_ptr(), image_bytes=img2.numel(), hd=args.small_net)
-        del img2
+    multi = multi_small = None
+    nets = [(args.seed, args.hd)] + ([(args.seed + 1000, args.small_net)] if args.small_net else [])
+    evs = []  # per net: list of per-device contexts
+    for seed, hd in nets:
+        if launch == "devices":
+            m = F.MultiEvaluator(F.Net.from_bytes(F.synthesize_net(seed, hd, 0)), devices)
+            if multi is None:
+                multi = m
+            else:
+                multi_small = m
+            evs.append([m.ctx(i) for i in range(len(devices))])
+        else:
+            dev = torch.device("cuda", local)
+            image = F.Net.from_bytes(F.synthesize_net(seed, hd, 0)).image() if rank == 0 else None
+            img = D.broadcast_image(image, dev) if dist_on else torch.from_numpy(image).to(dev)
+            torch.cuda.synchronize()
+            evs.append([F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=hd)])
+            del img
+    for e in evs[0]:
+        e.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
     t_net = time.time() - t0
 
-    # ---- inputs: this rank's shard, resident in HBM ----
+    # ---- inputs: one shard per GPU, resident in HBM ----
     t0 = time.time()
-    seed = D.shard_seed(args.seed, rank)
-    off = None
-    if args.workload == "positions":
-        pos = F.random_playouts(seed, args.positions, 0, 160, threads=threads)
-        board = boards_of(pos)
+    shards, host0 = [], None
+    for i, d in enumerate(devices):
+        g = rank if dist_on else i
+        pos, off = make_inputs(F, args, D.shard_seed(args.seed, g), threads)
+        if host0 is None:
+            host0 = (pos, off)
+        shards.append(Shard(torch, torch.device("cuda", d), pos, off, args.small_net))
+    pos, off = host0
+    board = boards_of(pos)
+    if not groups:
         rows = rows_scratch(board)
         workload = ("BASELINE config 2: random-playout positions (splitmix64, L~U[0,160]), from-scratch "
                     "accumulators, synthetic SFNNv5 net (HalfKAv2_hm, HD=%d)" % args.hd)
     else:
-        mode = F.PLAYOUT_PLIES if args.workload == "games" else F.PLAYOUT_CHILDREN
-        pos, off = F.random_playouts(seed + 1, args.games, 0, 160, mode=mode, threads=threads)
-        board = boards_of(pos)
         starts = off[:-1].astype(np.int64)
         has_base = np.ones(len(pos), dtype=bool)
         has_base[starts] = False
-        if args.workload == "games":
-            base_idx = np.arange(len(pos)) - 1
-        else:
-            base_idx = starts[np.repeat(np.arange(len(starts)), np.diff(off))]
+        base_idx = (np.arange(len(pos)) - 1 if args.workload == "games"
+                    else starts[np.repeat(np.arange(len(starts)), np.diff(off))])
         base_idx[~has_base] = 0
         rows = rows_incremental(board, board[base_idx], has_base)
         workload = ("BASELINE config %s: %d random-playout games per GPU, %s, synthetic SFNNv5 net (HD=%d)"
@@ -156,110 +272,123 @@ def main():
         workload += (f"; every position also through a second synthetic net of HD {args.small_net} "
                      f"(big + small net, both evaluated each step)")
     t_gen = time.time() - t0
-    npos = len(pos)
+    npos = shards[0].n
     pieces = (board != 0).sum(axis=1)
-    d_pos = torch.from_numpy(pos).to(dev)
-    d_off = torch.from_numpy(off.astype(np.int32)).to(dev) if off is not None else None
-    d_psqt = torch.zeros(npos, dtype=torch.int32, device=dev)
-    d_positional = torch.zeros(npos, dtype=torch.int32, device=dev)
-    d_small = torch.zeros(2, npos, dtype=torch.int32, device=dev) if ev_small else None
-    stream = torch.cuda.current_stream()
 
-    def run(e, ps, po):
-        if off is None:
-            e.eval_positions_device(d_pos.data_ptr(), npos, ps, po, stream.cuda_stream)
+    def run_net(k):
+        outs = [(s.psqt, s.positional) if k == 0 else (s.small[0], s.small[1]) for s in shards]
+        if launch == "devices":
+            m = multi if k == 0 else multi_small
+            if not groups:
+                m.eval_positions_device([s.pos.data_ptr() for s in shards], [s.n for s in shards],
+                                        [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs])
+            else:
+                m.eval_groups_device([s.pos.data_ptr() for s in shards], [s.off.data_ptr() for s in shards],
+                                     [s.ng for s in shards], [s.n for s in shards], gmode,
+                                     [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs])
         else:
-            e.eval_groups_device(d_pos.data_ptr(), d_off.data_ptr(), len(off) - 1, npos,
-                                 F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR, ps, po,
-                                 stream.cuda_stream)
+            s, e = shards[0], evs[k][0]
+            stream = torch.cuda.current_stream().cuda_stream
+            if not groups:
+                e.eval_positions_device(s.pos.data_ptr(), s.n, outs[0][0].data_ptr(), outs[0][1].data_ptr(), stream)
+            else:
+                e.eval_groups_device(s.pos.data_ptr(), s.off.data_ptr(), s.ng, s.n, gmode, outs[0][0].data_ptr(),
+                                     outs[0][1].data_ptr(), stream)
 
     def step():
-        run(ev, d_psqt.data_ptr(), d_positional.data_ptr())
-        if ev_small:
-            run(ev_small, d_small[0].data_ptr(), d_small[1].data_ptr())
+        for k in range(len(evs)):
+            run_net(k)
+
+    def sync_all():
+        for d in devices:
+            torch.cuda.synchronize(d)
+
+    def check_all():
+        for ctxs in evs:
+            for e in ctxs:
+                e.check()
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    ev.check()
-    if ev_small:
-        ev_small.check()
-        ev_small.set_timing(True)
-
-    ev.set_timing(True)
+    sync_all()
+    check_all()
+    for ctxs in evs:
+        ctxs[0].set_timing(True)
     if dist_on:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync_all()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync_all()
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    launches, ft_ms, stack_ms = ev.timing_read()
-    ev.set_timing(False)
-    ev.check()
+    launches, plan_ms, ft_ms, stack_ms = evs[0][0].timing_phases()
+    small_t = evs[1][0].timing_phases() if len(evs) > 1 else None
+    for ctxs in evs:
+        ctxs[0].set_timing(False)
+    check_all()
+    if dist_on:
+        elapsed_max = D.max_over_ranks(elapsed, torch.device("cuda", local))
+        tot = torch.tensor([float(sum(s.n for s in shards))], dtype=torch.float64, device=shards[0].dev)
+        dist.all_reduce(tot)
+        total_positions = float(tot.item())
+    else:
+        elapsed_max, total_positions = elapsed, float(sum(s.n for s in shards))
+    n_gpus = world if dist_on else len(devices)
+    assert n_gpus == args.gpus, (n_gpus, args.gpus)
+    value = total_positions * args.steps / elapsed_max
+
+    # ---- live kernel times (HIP events on the launch stream, device 0) ----
+    L = max(launches, 1)
+    plan_avg, ft_avg, stack_avg = plan_ms / L, ft_ms / L, stack_ms / L
+    bytes_per_launch = float(rows.sum()) * (2 * args.hd + 4 * PSQT_BUCKETS) + npos * (36 + 8)
+
+    # ---- results of device 0 to the host (outside the timed region) ----
+    psqt = shards[0].psqt.cpu().numpy()
+    positional = shards[0].positional.cpu().numpy()
+    gathered = None
+    if dist_on:
+        # evals gathered back to rank 0 over RCCL (north star "evals are gathered back"), timed on its own
+        dev = torch.device("cuda", local)
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        g_ps = D.gather_to_rank0(shards[0].psqt, dev)
+        g_po = D.gather_to_rank0(shards[0].positional, dev)
+        gms = (time.perf_counter() - tg) * 1e3
+        if rank == 0:
+            gathered = {"positions": int(g_ps.size), "gather_ms": round(gms, 3),
+                        "equals_sum_of_shards": bool(g_ps.size == g_po.size == int(total_positions))}
     small = None
-    if ev_small:
-        l2, f2, s2 = ev_small.timing_read()
-        ev_small.set_timing(False)
-        ev_small.check()
+    if args.small_net and rank == 0:
         # parity of the small net on a bounded sample against the oracle (test infrastructure)
         from oracle.oracle import OracleNet
         on2 = OracleNet(F.synthesize_net(args.seed + 1000, args.small_net, 0))
         k = min(npos, 200_000)
         ps2, po2, rc2 = on2.simd_eval_packed(pos[:k], threads=threads)
-        g2 = d_small[:, :k].cpu().numpy()
-        small = {"hd": args.small_net, "ft_kernel_avg_ms": round(f2 / max(l2, 1), 4),
-                 "stack_kernel_avg_ms": round(s2 / max(l2, 1), 4),
+        g2 = shards[0].small[:, :k].cpu().numpy()
+        l2, p2, f2, s2 = small_t
+        small = {"hd": args.small_net, "plan_avg_ms": round(p2 / max(l2, 1), 4),
+                 "ft_kernel_avg_ms": round(f2 / max(l2, 1), 4), "stack_kernel_avg_ms": round(s2 / max(l2, 1), 4),
                  "parity_spot_check": {"checked": k, "mismatches": int(((g2[0] != ps2) | (g2[1] != po2)).sum())
                                        if rc2 == 0 else None}}
-    if dist_on:
-        elapsed_max = D.max_over_ranks(elapsed, dev)
-        tot = torch.tensor([float(npos)], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot)
-        total_positions = float(tot.item())
-    else:
-        elapsed_max, total_positions = elapsed, float(npos)
-    value = total_positions * args.steps / elapsed_max
 
-    # ---- roofline of the dominant kernel (feature transformer) ----
-    # each feature row costs 2*HD bytes of FT weights + 4*PB bytes of PSQT
-    # weights; + 36 B position in + 8 B results out.
-    bytes_per_launch = float(rows.sum()) * (2 * args.hd + 4 * PSQT_BUCKETS) + npos * (36 + 8)
-    ft_avg_ms = ft_ms / max(launches, 1)
-    stack_avg_ms = stack_ms / max(launches, 1)
-    achieved_gbs = bytes_per_launch / (ft_avg_ms * 1e-3) / 1e9
-
-    # ---- results back to host (outside the timed region): parity spot check + CPU baseline ----
-    psqt = d_psqt.cpu().numpy()
-    positional = d_positional.cpu().numpy()
-    cpu = None
-    parity = None
-    gathered = None
-    if dist_on:
-        # Evals gathered back to rank 0 over RCCL (north star: "evals are gathered
-        # back"), outside the timed region: 8 B per position.
-        g_ps = D.gather_to_rank0(psqt, dev)
-        g_po = D.gather_to_rank0(positional, dev)
-        if rank == 0:
-            gathered = {"positions": int(g_ps.size), "equals_sum_of_shards": bool(g_ps.size == g_po.size
-                                                                                  == int(total_positions))}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    cpu, parity = None, None
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         from oracle.oracle import OracleNet  # cpu_baseline leg: oracle/nnue_cpu_simd.c is the timed CPU port
         from oracle.oracle import lib as olib
         isa = "AVX-512 VNNI" if olib.cpu_simd_isa512() else "AVX2"
         on = OracleNet(F.synthesize_net(args.seed, args.hd, 0))
         done, mism, t0 = 0, 0, time.perf_counter()
         chunk = 100_000
-        if off is not None:
-            gmode = F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR
+        if groups:
             ng = len(off) - 1
             g_per = max(1, int(chunk * ng / npos))
         g = 0
         while True:
-            if off is None:
+            if not groups:
                 lo = done % npos
                 hi = min(lo + chunk, npos)
                 ps, po, rc = on.simd_eval_packed(pos[lo:hi], threads=threads)
@@ -275,59 +404,87 @@ def main():
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
         cpu_el = time.perf_counter() - t0
-        how = ("from-scratch refresh per position" if off is None else
+        how = ("from-scratch refresh per position" if not groups else
                "incremental accumulators along the groups, refresh on own-king moves")
         cpu = {"value": done / cpu_el, "unit": "positions/s", "cores": threads, "kind": "port",
+               "cpu": {k: cpus[k] for k in ("model", "os_cpu_count", "affinity", "cgroup_quota", "omp_num_threads")},
                "sample": f"{done} positions of the same workload ({how}; {cpu_el:.1f} s wall on {threads} "
-                         f"threads; oracle/nnue_cpu_simd.c = Stockfish's {isa} NNUE code paths restated "
-                         f"(register-tiled accumulators, maddubs/VPDPBUSD affine), -O3; bit-identical to the "
-                         f"scalar oracle)"}
+                         f"threads = every core this process may use; oracle/nnue_cpu_simd.c = Stockfish's {isa} "
+                         f"NNUE code paths restated (register-tiled accumulators, maddubs/VPDPBUSD affine), -O3; "
+                         f"bit-identical to the scalar oracle)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
+    elif rank == 0 and launch == "devices":
+        # spot check of device 0's shard against the oracle (test infrastructure)
+        from oracle.oracle import OracleNet
+        on = OracleNet(F.synthesize_net(args.seed, args.hd, 0))
+        k = min(npos, 100_000)
+        ops, opo, rc = on.simd_eval_packed(pos[:k], threads=threads)
+        parity = {"checked": k, "mismatches": int(((ops != psqt[:k]) | (opo != positional[:k])).sum())}
 
-    # The host-buffer entry points (fnnue_eval_positions / _groups: host arrays in,
-    # host arrays out, PCIe both ways, host-side validation) — reported beside
-    # `value`, never as it (inputs resident in HBM is the contract).
+    # The host-buffer entry points (host arrays in and out over PCIe, validity
+    # checked on the device) — reported beside `value`, never as it.
     host_api = None
-    if world == 1 and not args.no_host_api:
-        ev.set_timing(False)
+    if not dist_on and not args.no_host_api:
         reps = 3
+        hpos = pos if launch != "devices" else np.concatenate([pos] * len(devices))
+        hoff = off
+        if groups and launch == "devices":
+            hoff = np.concatenate([off[:-1] + i * off[-1] for i in range(len(devices))] + [[off[-1] * len(devices)]])
+        target = multi if launch == "devices" else evs[0][0]
         t0 = time.perf_counter()
         for _ in range(reps):
-            if off is None:
-                hp, hq = ev.eval_positions(pos)
-            else:
-                hp, hq = ev.eval_groups(pos, off, F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR)
+            hp, hq = target.eval_positions(hpos) if not groups else target.eval_groups(hpos, hoff, gmode)
         host_el = time.perf_counter() - t0
-        host_api = {"value": npos * reps / host_el, "unit": "positions/s",
-                    "same_results": bool(np.array_equal(hp, psqt) and np.array_equal(hq, positional)),
+        host_api = {"value": len(hpos) * reps / host_el, "unit": "positions/s",
+                    "same_results": bool(np.array_equal(hp[:npos], psqt) and np.array_equal(hq[:npos], positional)),
                     "note": "host (pageable numpy) buffers through the C ABI: H2D 36 B + D2H 8 B per position "
-                            "over PCIe around the same kernels (validity checked on the device)"}
+                            "over PCIe around the same kernels"
+                            + (" (fnnue_multi: one host thread per GPU, results into disjoint slices)"
+                               if launch == "devices" else "")}
 
-    # roofline.traffic: PMC-measured bytes per launch of the same workload, from the
-    # committed profile (tools/profile.sh + tools/traffic.py -> profiles/traffic.json).
-    traffic, traffic_src, issue = None, None, None
-    tkey = f"{args.workload}:{args.ft_impl if off is None else 'groups'}:hd{args.hd}"
-    tpath = os.path.join(ROOT, "profiles", "traffic.json")
-    if os.path.exists(tpath):
-        entry = json.load(open(tpath)).get(tkey)
-        if entry:
-            traffic, traffic_src = entry["bytes_per_launch"], entry["source"]
-            if entry.get("valu_insts_per_launch"):
-                # The sliced FT moves ~2% of its algorithmic bytes through HBM; what bounds
-                # it is vector-instruction issue: SQ_INSTS_VALU per launch
-                # (committed PMC profile) over the live kernel time, against one
-                # 64-bit-encoded (VOP3/VOP3P/SDWA) wave64 VALU instruction per 4 cycles
-                # per SIMD at the 2.4 GHz spec clock (tools/diag/valu_bench.hip).
-                rate = entry["valu_insts_per_launch"] / (ft_avg_ms * 1e-3)
-                issue = {"unit": "VALU instr/s", "achieved": round(rate, -6), "peak": VALU_PEAK,
-                         "frac": round(rate / VALU_PEAK, 4), "source": traffic_src}
+    # ---- roofline: binding resource of the dominant kernel ----
+    impl = "sliced" if args.ft_impl == "sliced" else "gather"
+    main_k = MAIN_KERNEL[("groups" if groups else "positions", impl)]
+    counters, src, tree_ok = None, None, None
+    cpath = os.path.join(ROOT, "profiles", "counters.json")
+    if os.path.exists(cpath) and args.hd == 1024 and not args.small_net:
+        db = json.load(open(cpath))
+        counters = db.get("workloads", {}).get(args.workload)
+        src = db.get("source")
+        tree_ok = db.get("tree") == tree_hash()
+    kernels = {}
+    for name, t_ms in ((main_k, ft_avg), ("stack_kernel", stack_avg)):
+        rec = {"live_avg_ms": round(t_ms, 4)}
+        c = (counters or {}).get(name, {}).get("counters")
+        if c and t_ms > 0:
+            rec["fractions"] = resource_fractions(c, t_ms * 1e-3)
+            rec["profiled_avg_ms"] = round((counters[name].get("avg_ns") or 0) / 1e6, 4)
+        kernels[name] = rec
+    fr = kernels[main_k].get("fractions", {})
+    roofline = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    if fr:
+        bound = max(fr, key=lambda k: fr[k]["frac"])
+        b = fr[bound]
+        roofline.update(bound=bound, achieved=b["achieved"], peak=b["peak"], unit=b["unit"], frac=b["frac"],
+                        traffic=int(fr["hbm"]["bytes"]) if "hbm" in fr else None)
+    roofline.update({
+        "kernel": main_k, "kernel_avg_ms": round(ft_avg, 4), "plan_avg_ms": round(plan_avg, 4),
+        "stack_kernel_avg_ms": round(stack_avg, 4), "kernels": kernels,
+        "gather_equivalent_GBps": round(bytes_per_launch / (ft_avg * 1e-3) / 1e9, 1) if ft_avg > 0 else None,
+        "algorithmic_bytes_per_launch": int(bytes_per_launch),
+        "counters": {"source": src, "tree_matches": tree_ok},
+        "note": "frac = the largest of VALU-issue / LDS-busy / HBM fractions of the dominant kernel (counters per "
+                "launch from the committed profile of this tree, over the live kernel time here; peaks at the "
+                "2.4 GHz spec clock); gather_equivalent_GBps = SURVEY §8d algorithmic bytes (every feature row "
+                "read from memory) over the same time: the sliced kernels read rows from LDS tiles, so it may "
+                "exceed the 8 TB/s HBM peak"})
 
     if rank == 0:
         out = {
             "metric": METRIC,
             "value": value,
             "unit": "positions/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed_max * 1e3 / args.steps,
@@ -341,27 +498,14 @@ def main():
                 "positions_per_gpu": npos,
                 "mean_pieces": round(float(pieces.mean()), 3),
                 "hd": args.hd if not args.small_net else f"{args.hd}+{args.small_net}",
-                "parallelism": f"dp{world}",
-                "ft_impl": args.ft_impl if off is None else "groups",
+                "parallelism": f"dp{n_gpus}",
+                "launch": {"ranks": "torchrun: one process per GPU, RCCL broadcast of the net",
+                           "devices": "one process, fnnue_multi over %d GPUs (RCCL broadcast inside the C ABI)"
+                                      % n_gpus,
+                           "single": "one process, one GPU"}[launch],
+                "ft_impl": args.ft_impl if not groups else "groups",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved_gbs, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "issue": issue,
-                "kernel": {("positions", "sliced"): "ft_slices_kernel + plan_* (LDS-stationary FT)",
-                           ("positions", "gather"): "ft_scratch_kernel",
-                           ("groups", "sliced"): "ft_segments_kernel + seg_* plan (incremental on LDS tiles)",
-                           ("groups", "gather"): "ft_groups_kernel"}[("positions" if off is None else "groups",
-                                                                     args.ft_impl)],
-                "kernel_avg_ms": round(ft_avg_ms, 4),
-                "stack_kernel_avg_ms": round(stack_avg_ms, 4),
-                "algorithmic_bytes_per_launch": int(bytes_per_launch),
-            },
+            "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_spot_check": parity,
             "gathered": gathered,
@@ -370,9 +514,12 @@ def main():
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
         print(json.dumps(out), flush=True)
-    ev.close()
-    if ev_small:
-        ev_small.close()
+    for ctxs in evs:
+        for e in ctxs:
+            e.close()
+    for m in (multi, multi_small):
+        if m is not None:
+            m.close()
     if dist_on:
         dist.destroy_process_group()
 

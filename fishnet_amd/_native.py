@@ -89,6 +89,16 @@ SIGNATURES = {
     "fnnue_build_batch": ([_vp, C.c_char_p, _sz, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_perft_device": ([_vp, C.c_char_p, _i32, _P(_u64)], _i32),
     "fnnue_random_game": ([_u64, C.c_char_p, _u32, C.c_char_p, _sz, _P(_sz)], _i32),
+    "fnnue_multi_create": ([_vp, _P(_i32), _i32, _P(_vp)], _i32),
+    "fnnue_multi_free": ([_vp], None),
+    "fnnue_multi_size": ([_vp, _P(_i32)], _i32),
+    "fnnue_multi_ctx": ([_vp, _i32, _P(_vp)], _i32),
+    "fnnue_multi_eval_positions": ([_vp, _vp, _sz, _vp, _vp], _i32),
+    "fnnue_multi_eval_groups": ([_vp, _vp, _sz, _vp, _sz, _i32, _vp, _vp], _i32),
+    "fnnue_multi_eval_positions_device": ([_vp, _P(_vp), _P(_sz), _P(_vp), _P(_vp)], _i32),
+    "fnnue_multi_eval_groups_device": ([_vp, _P(_vp), _P(_vp), _P(_sz), _P(_sz), _i32, _P(_vp), _P(_vp)], _i32),
+    "fnnue_multi_sync": ([_vp], _i32),
+    "fnnue_partition_groups": ([_vp, _sz, _i32, _vp], _i32),
 }
 
 for _name, (_args, _res) in SIGNATURES.items():

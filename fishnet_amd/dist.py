@@ -63,20 +63,37 @@ def max_over_ranks(value: float, device) -> float:
     return float(t.item())
 
 
-def gather_to_rank0(local: np.ndarray, device):
-    """Concatenate every rank's 1-D int32 result array on rank 0 (None elsewhere)."""
+def gather_to_rank0(local, device):
+    """Every rank's 1-D int32 results concatenated on rank 0 (None elsewhere).
+
+    One dist.gather to rank 0 (RCCL over xGMI for "nccl"): each rank sends its
+    shard once, padded to the largest shard; nothing goes to the other ranks.
+    `local` is a numpy array or a tensor already on `device`."""
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size()
-    n = torch.tensor([local.size], dtype=torch.int64, device=device)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = local if isinstance(local, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(local, dtype=np.int32))
+    t = t.to(device=device, dtype=torch.int32).reshape(-1)
+    n = torch.tensor([t.numel()], dtype=torch.int64, device=device)
     sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    cap = int(max(s.item() for s in sizes))
-    padded = torch.zeros(cap, dtype=torch.int32, device=device)
-    padded[: local.size] = torch.from_numpy(np.ascontiguousarray(local, dtype=np.int32)).to(device)
-    parts = [torch.zeros(cap, dtype=torch.int32, device=device) for _ in range(world)]
-    dist.all_gather(parts, padded)
-    if dist.get_rank() != 0:
+    dist.all_gather(sizes, n)  # world x 8 bytes
+    sizes = [int(x.item()) for x in sizes]
+    cap = max(sizes)
+    if t.numel() < cap:
+        t = torch.cat([t, torch.zeros(cap - t.numel(), dtype=torch.int32, device=device)])
+    parts = [torch.empty(cap, dtype=torch.int32, device=device) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, parts, dst=0)
+    if rank != 0:
         return None
-    return np.concatenate([p[: int(s.item())].cpu().numpy() for p, s in zip(parts, sizes)])
+    return np.concatenate([p[:k].cpu().numpy() for p, k in zip(parts, sizes)])
+
+
+def shard_groups(off: np.ndarray, rank: int, world: int) -> tuple[int, int]:
+    """This rank's contiguous run of whole groups [g0, g1), balanced by position
+    count (fnnue_partition_groups; a game or a parent with its children is
+    never split across ranks)."""
+    from .nnue import partition_groups
+
+    cut = partition_groups(off, world)
+    return int(cut[rank]), int(cut[rank + 1])

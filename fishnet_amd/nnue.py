@@ -190,6 +190,96 @@ class Evaluator:
             self.close()
 
 
+class _BorrowedEvaluator(Evaluator):
+    """The context of one device of a MultiEvaluator (owned by it)."""
+
+    def __init__(self, handle: C.c_void_p, device: int):  # noqa: D401  (no ctx creation)
+        self._h = handle
+        self.device = device
+
+    def close(self) -> None:
+        self._h = C.c_void_p()
+
+
+def _ptrs(vals) -> C.Array:
+    return (C.c_void_p * len(vals))(*[C.c_void_p(v) for v in vals])
+
+
+def _sizes(vals) -> C.Array:
+    return (C.c_size_t * len(vals))(*vals)
+
+
+class MultiEvaluator:
+    """Several GPUs from one process (fnnue_multi_*): the net is RCCL-broadcast
+    from devices[0]; batches are sharded without a data-path collective.  The
+    reference's one-engine-per-core parallelism ([ref] src/main.rs:156-170)."""
+
+    def __init__(self, net: Net, devices):
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        N.check(N.lib.fnnue_multi_create(net.handle, devs, len(devices), C.byref(h)))
+        self._h = h
+        self.devices = list(devices)
+
+    def __len__(self) -> int:
+        return len(self.devices)
+
+    def ctx(self, i: int) -> Evaluator:
+        h = C.c_void_p()
+        N.check(N.lib.fnnue_multi_ctx(self._h, i, C.byref(h)))
+        return _BorrowedEvaluator(h, self.devices[i])
+
+    def eval_positions(self, pos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
+        n = pos.shape[0]
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_multi_eval_positions(self._h, N.ptr(pos), n, N.ptr(psqt), N.ptr(positional)))
+        return psqt, positional
+
+    def eval_groups(self, pos: np.ndarray, off: np.ndarray, mode: int = N.GROUP_CHAIN):
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        if len(off) < 1 or int(off[-1]) != pos.shape[0]:
+            raise ValueError("off must have >= 1 entry and end at the number of positions")
+        n = pos.shape[0]
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_multi_eval_groups(self._h, N.ptr(pos), n, N.ptr(off), len(off) - 1, mode,
+                                              N.ptr(psqt), N.ptr(positional)))
+        return psqt, positional
+
+    # device-resident shards: one pointer / count per device (asynchronous; then sync())
+    def eval_positions_device(self, d_pos, n, d_psqt, d_positional) -> None:
+        N.check(N.lib.fnnue_multi_eval_positions_device(self._h, _ptrs(d_pos), _sizes(n), _ptrs(d_psqt),
+                                                        _ptrs(d_positional)))
+
+    def eval_groups_device(self, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional) -> None:
+        N.check(N.lib.fnnue_multi_eval_groups_device(self._h, _ptrs(d_pos), _ptrs(d_off), _sizes(ngroups),
+                                                     _sizes(npos), mode, _ptrs(d_psqt), _ptrs(d_positional)))
+
+    def sync(self) -> None:
+        N.check(N.lib.fnnue_multi_sync(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) and self._h.value:
+            N.lib.fnnue_multi_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        if N is not None and getattr(N, "lib", None) is not None:
+            self.close()
+
+
+def partition_groups(off: np.ndarray, nparts: int) -> np.ndarray:
+    """Whole groups into nparts contiguous runs of about equal position counts
+    (fnnue_partition_groups): part k = groups [cut[k], cut[k + 1])."""
+    off = np.ascontiguousarray(off, dtype=np.uint32)
+    cut = np.zeros(nparts + 1, dtype=np.uint32)
+    N.check(N.lib.fnnue_partition_groups(N.ptr(off), len(off) - 1, nparts, N.ptr(cut)))
+    return cut
+
+
 def pos_from_fen(fen: str) -> np.ndarray:
     out = N.positions_array(1)
     N.check(N.lib.fnnue_pos_from_fen(fen.encode(), N.ptr(out)))
