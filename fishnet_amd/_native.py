@@ -83,6 +83,9 @@ SIGNATURES = {
     "fnnue_selftest_mfma": ([_i32], _i32),
     "fnnue_ctx_set_timing": ([_vp, _i32], _i32),
     "fnnue_ctx_set_ft_impl": ([_vp, _i32], _i32),
+    "fnnue_net_accumulator_bound": ([_vp, _P(C.c_int32)], _i32),
+    "fnnue_ctx_swar": ([_vp, _P(_i32), _P(C.c_int32)], _i32),
+    "fnnue_ctx_set_swar": ([_vp, _i32], _i32),
     "fnnue_ctx_timing_read": ([_vp, _P(_u32), _P(C.c_double), _P(C.c_double)], _i32),
     "fnnue_ctx_timing_phases": ([_vp, _P(_u32), _P(C.c_double), _P(C.c_double), _P(C.c_double)], _i32),
     "fnnue_build_batch_device": ([_vp, _vp, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz), _vp], _i32),

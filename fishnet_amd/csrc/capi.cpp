@@ -190,6 +190,23 @@ int name_invalid(int rc, const fnnue_pos* pos, size_t n) {
 
 // Derives the LDS-tile layout of the FT weights from the (just uploaded) image.
 int finish_upload(fnnue_ctx* c) {
+  // May ft_slices sum rows as SWAR words?  Decided from the weights on the
+  // device (they may come from an RCCL broadcast): a one-off host copy.
+  {
+    const ImageLayout L = image_layout(c->hd);
+    std::vector<int16_t> w, b;
+    try {
+      w.resize((size_t)kFeatures * c->hd);
+      b.resize(c->hd);
+    } catch (const std::bad_alloc&) {
+      return fail(FNNUE_E_OOM, "host allocation failed");
+    }
+    HIP_TRY(hipMemcpy(w.data(), c->image + L.ft_w, w.size() * 2, hipMemcpyDeviceToHost), "hipMemcpy(ft weights)");
+    HIP_TRY(hipMemcpy(b.data(), c->image + L.ft_bias, b.size() * 2, hipMemcpyDeviceToHost), "hipMemcpy(ft bias)");
+    c->acc_bound = accumulator_bound(w.data(), b.data(), c->hd);
+    const char* env = std::getenv("FNNUE_SWAR");
+    c->plan.swar = c->acc_bound < 32768 && !(env && env[0] == '0');
+  }
   if (std::getenv("FNNUE_DEBUG_SKIP_RELAYOUT")) {  // diagnostics only: gather path without tiles
     c->ft_impl = FNNUE_FT_GATHER;
     return FNNUE_OK;
@@ -400,6 +417,27 @@ void fnnue_ctx_free(fnnue_ctx* ctx) { ctx_destroy(ctx); }
 int fnnue_ctx_set_ft_impl(fnnue_ctx* ctx, int impl) {
   if (!ctx || (impl != FNNUE_FT_SLICED && impl != FNNUE_FT_GATHER)) return fail(FNNUE_E_ARG, "bad ft impl");
   ctx->ft_impl = impl;
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_swar(const fnnue_ctx* ctx, int* enabled, int32_t* bound) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (enabled) *enabled = ctx->plan.swar ? 1 : 0;
+  if (bound) *bound = ctx->acc_bound;
+  return FNNUE_OK;
+}
+
+int fnnue_ctx_set_swar(fnnue_ctx* ctx, int enable) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (enable && ctx->acc_bound >= 32768)
+    return fail(FNNUE_E_ARCH, "accumulator bound " + std::to_string(ctx->acc_bound) + " >= 2^15: SWAR rows not exact");
+  ctx->plan.swar = enable != 0;
+  return FNNUE_OK;
+}
+
+int fnnue_net_accumulator_bound(const fnnue_net* net, int32_t* bound) {
+  if (!net || !bound) return fail(FNNUE_E_ARG, "null argument");
+  *bound = accumulator_bound(net->net.ft_w.data(), net->net.ft_bias.data(), net->net.hd);
   return FNNUE_OK;
 }
 

@@ -313,6 +313,8 @@ __device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4&
 // item, because the bucket changes along a segment (kPsqt: slice 0 only).
 // Then the wave walks the longest segment of the pass; finished items turn
 // their rows into the zero row and their stores out of range (dropped).
+constexpr int kDbufStride = 9;  // records per item in the per-wave LDS buffer (8 + 1 padding)
+
 template <int HD, bool kStar, bool kPsqt>
 __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
                                          int q, uint32_t n, const char* lbase, u16x4 b_lo, u16x4 b_hi, int krow,
@@ -365,7 +367,10 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drec_rsrc, k < rec.y ? rbase + 16u * k : 32u * n, 0, 0);
     return make_uint4(v.x, v.y, v.z, v.w);
   };
-  uint4* db = dbuf + 8 * it_in_wave;
+  // 9 records of stride per item (one padding record): the two items of a
+  // ds_read_b96 lane group ({0-3,20-23}: items 0 and 1; banks (a/4) mod 32)
+  // then read records 144 B apart, 4 banks, instead of 128 B = the same banks.
+  uint4* db = dbuf + kDbufStride * it_in_wave;
   const uint32_t nb = __builtin_amdgcn_readfirstlane((maxL - 1 + 7) / 8);  // batches, wave-uniform
 #ifndef SEG_PREFETCH
 #define SEG_PREFETCH 1
@@ -427,7 +432,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   __shared__ uint4 img[kTileU4];
   __shared__ int32_t ptile[kTileRows * kPsqtBuckets];
   __shared__ uint2 lbuf[16][64];
-  __shared__ uint4 dbuf[16][64];  // per wave: 8 positions' delta records of its 8 items
+  __shared__ uint4 dbuf[16][8 * kDbufStride];  // per wave: 8 positions' delta records of its 8 items
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
 // values, and slices != 0 issue their PSQT store out of the buffer's bounds
 // (dropped by the hardware).  A store skipped on some path would make hipcc's
 // vmcnt bookkeeping wait for every store before the next pass's rows.
-template <int HD>
+template <int HD, bool kSwar>
 __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
                                            int q, const char* base, u16x4 b_lo, u16x4 b_hi, int krow,
                                            const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
@@ -139,7 +139,11 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     e[4 * m + 3] = v.w;
   }
   u16x4 lo = b_lo, hi = b_hi;
-  rows_sum(maxn - 1, e, base, lo, hi);  // maxn - 1 rows (own king in the bias); wave-uniform, straight-line cases
+  rows_sum<kSwar>(maxn - 1, e, base, lo, hi);  // maxn - 1 rows (own king in the bias); wave-uniform, straight-line
+  if constexpr (kSwar) {
+    lo = swar_unpack4(lo);
+    hi = swar_unpack4(hi);
+  }
   // (rec & 0xFFFFFF) = 2 * slot + half: times HD/2 it is the offset of the
   // item's half of row `slot` of x.
   const uint32_t xoff = (rec & 0xFFFFFFu) * (HD / 2) + 32 * s + 4 * q;
@@ -175,8 +179,9 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; records and
 // lists are fetched two passes ahead while the current pass reads the LDS tile.
 // Items of a unit are sorted by piece count, so a pass's longest list is that
-// of its item 7 (clamped into the unit).
-template <int HD>
+// of its item 7 (clamped into the unit).  kSwar: the tile is converted to SWAR
+// words on its way into LDS and rows are summed as 32-bit words (swar_word).
+template <int HD, bool kSwar>
 __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict__ tiles,
                                                          const int16_t* __restrict__ ftb,
                                                          const uint32_t* __restrict__ ctr,
@@ -237,7 +242,11 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   PassFetch fb = fetch_pass(items_rsrc, flist_rsrc, base + 128, last, lane, it_in_wave);
 #pragma unroll
   for (int k = 0; k < kTileLoads; ++k)
-    if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
+    if ((int)threadIdx.x + 1024 * k < kTileU4) {
+      uint4 v = t[k];
+      if constexpr (kSwar) v = make_uint4(swar_word(v.x), swar_word(v.y), swar_word(v.z), swar_word(v.w));
+      img[threadIdx.x + 1024 * k] = v;
+    }
   if (s == 0) {
     uint4* pdst = reinterpret_cast<uint4*>(ptile);
 #pragma unroll
@@ -249,23 +258,25 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   __syncthreads();
   {  // the own-king row (every item of the unit has it) joins the bias
     const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
-    const u32x2 klo = __builtin_shufflevector(kv, kv, 0, 1), khi = __builtin_shufflevector(kv, kv, 2, 3);
-    b_lo += __builtin_bit_cast(u16x4, klo);
-    b_hi += __builtin_bit_cast(u16x4, khi);
+    if constexpr (kSwar) {
+      b_lo = swar_words(b_lo);
+      b_hi = swar_words(b_hi);
+    }
+    accum_row<kSwar>(kv, b_lo, b_hi);
   }
   while (base < u.z) {
     const PassFetch cur = fa;
 #ifndef FT_EXP_REUSE_LIST
     fa = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
 #endif
-    slice_pass<HD>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
+    slice_pass<HD, kSwar>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
     base += 128;
     if (base >= u.z) break;
     const PassFetch cur2 = fb;
 #ifndef FT_EXP_REUSE_LIST
     fb = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
 #endif
-    slice_pass<HD>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
+    slice_pass<HD, kSwar>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
     base += 128;
   }
 }
@@ -280,9 +291,14 @@ template <int HD>
 hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint32_t max_units, hipStream_t stream) {
   constexpr int S = HD / 64;
   const uint32_t groups = (max_units + 7) / 8;
-  hipLaunchKernelGGL((ft_slices_kernel<HD>), dim3(groups * 8 * S), dim3(1024), 0, stream,
-                     (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
-                     P.psqt_part, x);
+  if (P.swar)
+    hipLaunchKernelGGL((ft_slices_kernel<HD, true>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+                       (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
+                       P.psqt_part, x);
+  else
+    hipLaunchKernelGGL((ft_slices_kernel<HD, false>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+                       (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
+                       P.psqt_part, x);
   return hipGetLastError();
 }
 

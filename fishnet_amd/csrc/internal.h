@@ -34,6 +34,7 @@ struct fnnue_ctx {
   int32_t* d_positional = nullptr;
   size_t stage_cap = 0, off_cap = 0;
   int ft_impl = FNNUE_FT_SLICED;
+  int32_t acc_bound = 0;       // accumulator_bound of the net (SWAR rows allowed below 2^15)
   fnnue::SlicedPlan plan{};
   fnnue::SegPlan seg{};                // incremental sliced path for groups (allocated on first use)
   bool timing = false;

@@ -51,6 +51,7 @@ struct SlicedPlan {
   uint16_t* flist;   // [2 * chunk][32] feature rows relative to the king block
   uint32_t* perm;    // [chunk] bucket-sorted slot -> position index
   int32_t* psqt_part;// [chunk][2] per-slot PSQT sums of the stm / nstm perspective
+  bool swar;          // ft_slices may sum rows as SWAR words (accumulator_bound < 2^15)
 };
 size_t sliced_tiles_bytes(uint32_t hd);
 size_t sliced_ctr_words();

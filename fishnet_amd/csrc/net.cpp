@@ -1,7 +1,10 @@
 // net.cpp — .nnue parsing/writing, synthetic nets and the device image.
 #include "net.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <vector>
 #include <cstring>
 
 #include "../../include/fnnue.h"
@@ -255,6 +258,30 @@ void pack_image(const Net& net, uint8_t* dst) {
     std::memcpy(dst + L.w2 + (size_t)b * kL3, s.w2, kL3);
     std::memcpy(dst + L.b2 + (size_t)b * 4, &s.b2, 4);
   }
+}
+
+int32_t accumulator_bound(const int16_t* ft_w, const int16_t* ft_bias, uint32_t hd) {
+  constexpr int kRows = kFeatures / 32;  // rows per king block (704)
+  const uint32_t ncol = hd / 2;          // even columns
+  int64_t worst = 0;
+  std::vector<int32_t> mag((size_t)ncol * kRows);  // [even column][row], |w|
+  for (int kb = 0; kb < 32; ++kb) {
+    // own-king row of king block kb: plane 10, oriented king square on files e-h
+    // (KingBuckets is a bijection kb <-> oriented square; upstream half_ka_v2_hm.h)
+    const int krow = 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3));
+    const int16_t* blk = ft_w + (size_t)kb * kRows * hd;
+    for (int r = 0; r < kRows; ++r)
+      for (uint32_t c = 0; c < ncol; ++c)
+        mag[(size_t)c * kRows + r] = r == krow ? 0 : std::abs((int32_t)blk[(size_t)r * hd + 2 * c]);
+    for (uint32_t c = 0; c < ncol; ++c) {
+      int32_t* m = mag.data() + (size_t)c * kRows;
+      std::nth_element(m, m + 31, m + kRows, std::greater<int32_t>());
+      int64_t b = std::abs((int32_t)ft_bias[2 * c] + (int32_t)blk[(size_t)krow * hd + 2 * c]);
+      for (int k = 0; k < 31; ++k) b += m[k];
+      worst = std::max(worst, b);
+    }
+  }
+  return (int32_t)std::min<int64_t>(worst, INT32_MAX);
 }
 
 }  // namespace fnnue

@@ -60,4 +60,12 @@ struct ImageLayout {
 ImageLayout image_layout(uint32_t hd);
 void pack_image(const Net& net, uint8_t* dst);  // dst has image_layout(hd).total bytes
 
+// Largest possible |true int32 sum| of an even ("low") accumulator column over
+// every reachable accumulator: per king block kb and even column j,
+// |bias_j + w[own king row][j]| + the 31 largest |w[r][j]| of the other rows
+// of kb (a position has at most 31 pieces besides the perspective's king).
+// Below 2^15 the feature transformer may sum column pairs as 32-bit words
+// (ft_slices' SWAR rows) and still be bit-exact.
+int32_t accumulator_bound(const int16_t* ft_w, const int16_t* ft_bias, uint32_t hd);
+
 }  // namespace fnnue

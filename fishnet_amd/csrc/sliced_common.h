@@ -367,11 +367,39 @@ __device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word
 // instead of draining it.
 constexpr int kRowDepth = 4 * FT_DEPTH;
 
+// SWAR rows (ft_slices when the net allows it, accumulator_bound in net.h):
+// a 32-bit word holding the int16 columns (c, c+1) as l + 65536 * h with l
+// SIGNED, so that 32-bit adds of such words sum both columns at once (one VOP2
+// v_add_u32 per word instead of a VOP3P v_pk_add_u16, which issues at ~1.75x
+// its cost).  The sum is exact mod 2^32; while the true sum of column c stays
+// within int16 range its low half is that sum and the high half, after the
+// low half's sign is taken back out (swar_unpack), is column c+1's sum mod
+// 2^16 — the int16 wraparound of upstream's accumulator.
+__device__ __forceinline__ uint32_t swar_word(uint32_t packed) { return packed - ((packed & 0x8000u) << 1); }
+__device__ __forceinline__ uint32_t swar_unpack(uint32_t w) {
+  const uint32_t h = w - (uint32_t)(int32_t)(int16_t)(uint16_t)w;  // low 16 bits zero
+  return h | (w & 0xFFFFu);
+}
+__device__ __forceinline__ u16x4 swar_words(u16x4 v) {
+  const u32x2 w = __builtin_bit_cast(u32x2, v);
+  return __builtin_bit_cast(u16x4, u32x2{swar_word(w.x), swar_word(w.y)});
+}
+__device__ __forceinline__ u16x4 swar_unpack4(u16x4 v) {
+  const u32x2 w = __builtin_bit_cast(u32x2, v);
+  return __builtin_bit_cast(u16x4, u32x2{swar_unpack(w.x), swar_unpack(w.y)});
+}
+
+template <bool kSwar = false>
 __device__ __forceinline__ void accum_row(const u32x4& v, u16x4& lo, u16x4& hi) {
   const u32x2 a = __builtin_shufflevector(v, v, 0, 1);
   const u32x2 b = __builtin_shufflevector(v, v, 2, 3);
-  lo += __builtin_bit_cast(u16x4, a);
-  hi += __builtin_bit_cast(u16x4, b);
+  if constexpr (kSwar) {
+    lo = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, lo) + a);
+    hi = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, hi) + b);
+  } else {
+    lo += __builtin_bit_cast(u16x4, a);
+    hi += __builtin_bit_cast(u16x4, b);
+  }
 }
 
 template <int NR, int R = 0>
@@ -382,31 +410,33 @@ __device__ __forceinline__ void rows1_head(const uint32_t (&e)[16], const char* 
   }
 }
 
-template <int NR, int R = 0>
+template <int NR, bool kSwar, int R = 0>
 __device__ __forceinline__ void rows1_step(const uint32_t (&e)[16], const char* base, u32x4 (&v)[kRowDepth],
                                            u16x4& lo, u16x4& hi) {
   if constexpr (R < NR) {
-    accum_row(v[R % kRowDepth], lo, hi);
+    accum_row<kSwar>(v[R % kRowDepth], lo, hi);
     if constexpr (R + kRowDepth < NR) v[R % kRowDepth] = *row_addr(base, e[(R + kRowDepth) >> 1], (R + kRowDepth) & 1);
-    rows1_step<NR, R + 1>(e, base, v, lo, hi);
+    rows1_step<NR, kSwar, R + 1>(e, base, v, lo, hi);
   }
 }
 
 // Exactly NR rows (a pass's longest list, not rounded up: rounding to groups of
 // 4 cost 7 % padding rows, 2 % of the kernel), kRowDepth rows in flight,
 // branch-free straight-line code per row count.
-template <int NR>
+template <int NR, bool kSwar>
 __device__ __forceinline__ void rows_exact(const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
   u32x4 v[kRowDepth];
   rows1_head<NR>(e, base, v);
-  rows1_step<NR>(e, base, v, lo, hi);
+  rows1_step<NR, kSwar>(e, base, v, lo, hi);
 }
 
-// Sums the first `nrows` (wave-uniform, <= 32) rows of the feature list e.
+// Sums the first `nrows` (wave-uniform, <= 32) rows of the feature list e
+// (kSwar: rows and accumulator in SWAR words, see swar_word).
+template <bool kSwar = false>
 __device__ __forceinline__ void rows_sum(int nrows, const uint32_t (&e)[16], const char* base, u16x4& lo, u16x4& hi) {
   switch (nrows) {
 #define FNNUE_ROWS_CASE(k) \
-  case k: rows_exact<k>(e, base, lo, hi); break;
+  case k: rows_exact<k, kSwar>(e, base, lo, hi); break;
     FNNUE_ROWS_CASE(1) FNNUE_ROWS_CASE(2) FNNUE_ROWS_CASE(3) FNNUE_ROWS_CASE(4) FNNUE_ROWS_CASE(5)
     FNNUE_ROWS_CASE(6) FNNUE_ROWS_CASE(7) FNNUE_ROWS_CASE(8) FNNUE_ROWS_CASE(9) FNNUE_ROWS_CASE(10)
     FNNUE_ROWS_CASE(11) FNNUE_ROWS_CASE(12) FNNUE_ROWS_CASE(13) FNNUE_ROWS_CASE(14) FNNUE_ROWS_CASE(15)

@@ -53,6 +53,12 @@ class Net:
         N.check(N.lib.fnnue_net_info(self._h, C.byref(hd), C.byref(fh), C.byref(desc)))
         return hd.value, fh.value, desc.value.decode(errors="replace")
 
+    def accumulator_bound(self) -> int:
+        """Largest possible |sum| of an even accumulator column (< 2^15: SWAR rows exact)."""
+        b = C.c_int32()
+        N.check(N.lib.fnnue_net_accumulator_bound(self._h, C.byref(b)))
+        return b.value
+
     def image(self) -> np.ndarray:
         size = C.c_size_t()
         N.check(N.lib.fnnue_net_image_size(self._h, C.byref(size)))
@@ -164,6 +170,15 @@ class Evaluator:
     def set_ft_impl(self, impl: int) -> None:
         """FT_SLICED (default, LDS-stationary tiles) or FT_GATHER (per-position row gather)."""
         N.check(N.lib.fnnue_ctx_set_ft_impl(self._h, impl))
+
+    def swar(self) -> tuple[bool, int]:
+        """(SWAR row sums on, the net's accumulator bound)."""
+        e, b = C.c_int(), C.c_int32()
+        N.check(N.lib.fnnue_ctx_swar(self._h, C.byref(e), C.byref(b)))
+        return bool(e.value), b.value
+
+    def set_swar(self, enable: bool) -> None:
+        N.check(N.lib.fnnue_ctx_set_swar(self._h, 1 if enable else 0))
 
     def set_timing(self, enable: bool) -> None:
         N.check(N.lib.fnnue_ctx_set_timing(self._h, 1 if enable else 0))

@@ -252,6 +252,16 @@ int fnnue_selftest_mfma(int device);
 #define FNNUE_FT_SLICED 0
 #define FNNUE_FT_GATHER 1
 int fnnue_ctx_set_ft_impl(fnnue_ctx *ctx, int impl);
+/* SWAR row sums in the sliced feature transformer: pairs of int16 columns
+ * summed as 32-bit words.  Exact whenever no reachable
+ * accumulator's even column leaves int16 range; the library checks that from
+ * the weights (fnnue_net_accumulator_bound < 32768) and turns SWAR on by
+ * itself (FNNUE_SWAR=0 in the environment keeps it off).  Results are
+ * identical either way; set_swar(1) fails with FNNUE_E_ARCH on a net whose
+ * bound does not allow it. */
+int fnnue_net_accumulator_bound(const fnnue_net *net, int32_t *bound);
+int fnnue_ctx_swar(const fnnue_ctx *ctx, int *enabled, int32_t *bound);
+int fnnue_ctx_set_swar(fnnue_ctx *ctx, int enable);
 
 /* Kernel timing with HIP events on the launch stream: when enabled, every
  * chunk launched by a *_device call records events around the feature-

@@ -393,3 +393,29 @@ def test_device_calls_on_two_streams(ev_cache):
         idx = np.arange(0, len(pos), 13)
         ops, opo, rc = on.eval_packed(pos[idx], threads=8)
         assert np.array_equal(ps.cpu().numpy()[idx], ops) and np.array_equal(po.cpu().numpy()[idx], opo)
+
+
+@pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (6, 2048, 0), (8, 1536, N.SYNTH_LEB128)])
+def test_swar_rows_match_packed_rows(ev_cache, seed, hd, flags):
+    """ft_slices with SWAR row sums (32-bit words, enabled from the accumulator
+    bound) == packed int16 row sums == oracle; a net whose bound forbids SWAR
+    refuses it."""
+    ev, on = ev_cache(seed, hd, flags)
+    on_swar, bound = ev.swar()
+    assert on_swar and bound < 32768
+    pos = F.random_playouts(seed + 60, 40000, threads=8)
+    a = ev.eval_positions(pos)
+    ev.set_swar(False)
+    try:
+        b = ev.eval_positions(pos)
+    finally:
+        ev.set_swar(True)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    idx = np.arange(0, len(pos), 5)
+    ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+    assert np.array_equal(a[0][idx], ops) and np.array_equal(a[1][idx], opo)
+    evw, _ = ev_cache(3, 1024, N.SYNTH_WRAP)
+    assert evw.swar()[0] is False
+    with pytest.raises(F.FnnueError) as e:
+        evw.set_swar(True)
+    assert e.value.name == "FNNUE_E_ARCH"

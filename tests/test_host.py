@@ -187,3 +187,14 @@ def test_device_entry_points_fail_cleanly_without_gpu():
     assert e.value.name == "FNNUE_E_DEVICE"
     with pytest.raises(F.FnnueError):
         F.selftest_mfma(0)
+
+
+def test_accumulator_bound_decides_swar():
+    """SWAR row sums (ft_slices) are exact only if no reachable accumulator's
+    even column leaves int16 range: realistic synthetic nets qualify, the
+    int16-wrap stress net does not (the library then keeps packed adds)."""
+    import fishnet_amd as F
+    b = F.Net.from_bytes(F.synthesize_net(1, 1024, 0)).accumulator_bound()
+    assert 0 < b < 32768
+    w = F.Net.from_bytes(F.synthesize_net(3, 1024, N.SYNTH_WRAP)).accumulator_bound()
+    assert w >= 32768
