@@ -38,11 +38,11 @@ FOCUS = ("ft_slices_kernel", "ft_segments_kernel", "stack_kernel", "ft_scratch_k
 
 
 def tree_hash() -> str:
-    """sha256 over the device sources of libfnnue.so (what the kernel counters depend on)."""
+    """sha256 over the sources of the evaluation kernels (what their counters depend on)."""
     h = hashlib.sha256()
     src = os.path.join(ROOT, "fishnet_amd", "csrc")
-    dev_headers = [os.path.join(src, f) for f in ("device_common.h", "sliced_common.h", "kernels.h")]
-    for f in sorted(glob.glob(os.path.join(src, "*.hip")) + dev_headers):
+    files = ("kernels.hip", "ft_sliced.hip", "ft_segments.hip", "device_common.h", "sliced_common.h", "kernels.h")
+    for f in sorted(os.path.join(src, f) for f in files):
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
