@@ -23,7 +23,9 @@ SYNTH_LEB128, SYNTH_WRAP, SYNTH_FC1_PAD = 1, 2, 4
 GROUP_CHAIN, GROUP_STAR = 0, 1
 FT_SLICED, FT_GATHER = 0, 1
 PLAYOUT_FINAL, PLAYOUT_PLIES, PLAYOUT_CHILDREN = 0, 1, 2
+VARIANT_CHESS, VARIANT_CRAZYHOUSE, VARIANT_ATOMIC = 0, 1, 2
 POS_BYTES = 36
+VPOS_BYTES = 48
 
 
 class FnnueError(RuntimeError):
@@ -102,6 +104,14 @@ SIGNATURES = {
     "fnnue_multi_eval_groups_device": ([_vp, _P(_vp), _P(_vp), _P(_sz), _P(_sz), _i32, _P(_vp), _P(_vp)], _i32),
     "fnnue_multi_sync": ([_vp], _i32),
     "fnnue_partition_groups": ([_vp, _sz, _i32, _vp], _i32),
+    "fnnue_net_load_variant": ([C.c_char_p, _i32, _P(_vp)], _i32),
+    "fnnue_net_load_variant_mem": ([_vp, _sz, _i32, _P(_vp)], _i32),
+    "fnnue_net_variant": ([_vp, _P(_i32)], _i32),
+    "fnnue_net_synthesize_variant": ([_u64, _u32, _i32, _u32, _P(_vp), _P(_sz)], _i32),
+    "fnnue_vpos_from_fen": ([_i32, C.c_char_p, _vp], _i32),
+    "fnnue_random_vpositions": ([_u64, _i32, _sz, _u32, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
+    "fnnue_eval_vpositions": ([_vp, _vp, _sz, _vp, _vp], _i32),
+    "fnnue_eval_vpositions_device": ([_vp, _vp, _sz, _vp, _vp, _vp], _i32),
 }
 
 for _name, (_args, _res) in SIGNATURES.items():
@@ -125,3 +135,7 @@ def ptr(a) -> int | None:
 
 def positions_array(n: int) -> np.ndarray:
     return np.zeros((n, POS_BYTES), dtype=np.uint8)
+
+
+def vpositions_array(n: int) -> np.ndarray:
+    return np.zeros((n, VPOS_BYTES), dtype=np.uint8)

@@ -72,8 +72,8 @@ void ctx_destroy(fnnue_ctx* c) {
   delete c;
 }
 
-NetPtrs make_ptrs(uint8_t* img, uint32_t hd) {
-  const ImageLayout L = image_layout(hd);
+NetPtrs make_ptrs(uint8_t* img, uint32_t hd, uint32_t nfeat) {
+  const ImageLayout L = image_layout(hd, nfeat);
   NetPtrs p;
   p.ft_w = reinterpret_cast<const int16_t*>(img + L.ft_w);
   p.ft_bias = reinterpret_cast<const int16_t*>(img + L.ft_bias);
@@ -88,17 +88,21 @@ NetPtrs make_ptrs(uint8_t* img, uint32_t hd) {
 }
 
 // Allocates everything except the image contents.
-int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
+int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant) {
   *out = nullptr;
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0) return fail(FNNUE_E_DEVICE, "no HIP device available");
   if (device < 0 || device >= ndev) return fail(FNNUE_E_DEVICE, "device ordinal out of range");
   if (!kernels_support_hd(hd)) return fail(FNNUE_E_ARCH, "no kernel instantiation for hd " + std::to_string(hd));
+  if (variant != kVariantChess && hd != 256 && hd != 512 && hd != 1024)
+    return fail(FNNUE_E_ARCH, "variant nets: hd 256, 512 or 1024, not " + std::to_string(hd));
   std::unique_ptr<fnnue_ctx, void (*)(fnnue_ctx*)> c(new (std::nothrow) fnnue_ctx, ctx_destroy);
   if (!c) return fail(FNNUE_E_OOM, "host allocation failed");
   c->device = device;
   c->hd = hd;
+  c->variant = variant;
+  c->nfeat = features_of(variant);
   c->chunk = chunk_for_hd(hd);
   if (const char* s = std::getenv("FNNUE_CHUNK")) {  // experiment knob: smaller launches (multiple of 1024)
     const unsigned long v = std::strtoul(s, nullptr, 10) & ~1023ul;
@@ -106,16 +110,18 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
   }
   const uint32_t chunk = c->chunk;
   DeviceGuard g(device);
-  c->image_bytes = image_layout(hd).total;
+  c->image_bytes = image_layout(hd, c->nfeat).total;
   if (hipMalloc(&c->image, c->image_bytes) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (net image)");
   if (hipMalloc(&c->x, (size_t)chunk * hd) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
   if (hipMalloc(&c->bucket, chunk) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (workspace)");
   if (hipMalloc(&c->err, sizeof(uint32_t)) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (error word)");
   HIP_TRY(hipMemset(c->err, 0, sizeof(uint32_t)), "hipMemset");
   SlicedPlan& P = c->plan;
-  if (hipMalloc(&P.tiles, sliced_tiles_bytes(hd)) != hipSuccess ||
-      hipMalloc(&P.ctr, sliced_ctr_words() * sizeof(uint32_t)) != hipSuccess ||
-      hipMalloc(&P.units, (size_t)std::max(sliced_max_units(chunk), seg_max_units(chunk)) * 16) != hipSuccess ||
+  const size_t tiles = variant == kVariantChess ? sliced_tiles_bytes(hd) : variant_tiles_bytes(hd, variant);
+  const size_t units = std::max({sliced_max_units(chunk), seg_max_units(chunk), variant_max_units(chunk)});
+  if (hipMalloc(&P.tiles, tiles) != hipSuccess ||
+      hipMalloc(&P.ctr, std::max(sliced_ctr_words(), variant_ctr_words()) * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.units, units * 16) != hipSuccess ||
       hipMalloc(&P.items, (size_t)2 * chunk * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&P.flist, (size_t)2 * chunk * 32 * sizeof(uint16_t)) != hipSuccess ||
       hipMalloc(&P.perm, (size_t)chunk * sizeof(uint32_t)) != hipSuccess ||
@@ -125,7 +131,7 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out) {
     c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
   HIP_TRY(hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming), "hipEventCreate");
-  c->ptrs = make_ptrs(c->image, hd);
+  c->ptrs = make_ptrs(c->image, hd, c->nfeat);
   *out = c.release();
   return FNNUE_OK;
 }
@@ -137,7 +143,8 @@ int ensure_stage(fnnue_ctx* c, size_t npos, size_t noff) {
     c->d_pos = nullptr;
     c->d_psqt = c->d_positional = nullptr;
     c->stage_cap = 0;
-    if (hipMalloc(&c->d_pos, npos * sizeof(fnnue_pos)) != hipSuccess ||
+    // sized for the larger record (fnnue_vpos) so both entry points share it
+    if (hipMalloc(&c->d_pos, npos * sizeof(fnnue_vpos)) != hipSuccess ||
         hipMalloc(&c->d_psqt, npos * sizeof(int32_t)) != hipSuccess ||
         hipMalloc(&c->d_positional, npos * sizeof(int32_t)) != hipSuccess)
       return fail(FNNUE_E_OOM, "device allocation (staging)");
@@ -193,17 +200,17 @@ int finish_upload(fnnue_ctx* c) {
   // May ft_slices sum rows as SWAR words?  Decided from the weights on the
   // device (they may come from an RCCL broadcast): a one-off host copy.
   {
-    const ImageLayout L = image_layout(c->hd);
+    const ImageLayout L = image_layout(c->hd, c->nfeat);
     std::vector<int16_t> w, b;
     try {
-      w.resize((size_t)kFeatures * c->hd);
+      w.resize((size_t)c->nfeat * c->hd);
       b.resize(c->hd);
     } catch (const std::bad_alloc&) {
       return fail(FNNUE_E_OOM, "host allocation failed");
     }
     HIP_TRY(hipMemcpy(w.data(), c->image + L.ft_w, w.size() * 2, hipMemcpyDeviceToHost), "hipMemcpy(ft weights)");
     HIP_TRY(hipMemcpy(b.data(), c->image + L.ft_bias, b.size() * 2, hipMemcpyDeviceToHost), "hipMemcpy(ft bias)");
-    c->acc_bound = accumulator_bound(w.data(), b.data(), c->hd);
+    c->acc_bound = accumulator_bound(w.data(), b.data(), c->hd, c->variant);
     const char* env = std::getenv("FNNUE_SWAR");
     c->plan.swar = c->acc_bound < 32768 && !(env && env[0] == '0');
   }
@@ -211,7 +218,10 @@ int finish_upload(fnnue_ctx* c) {
     c->ft_impl = FNNUE_FT_GATHER;
     return FNNUE_OK;
   }
-  HIP_TRY(launch_relayout_sliced(c->hd, c->ptrs, c->plan.tiles, c->stream), "relayout launch");
+  if (c->variant == kVariantChess)
+    HIP_TRY(launch_relayout_sliced(c->hd, c->ptrs, c->plan.tiles, c->stream), "relayout launch");
+  else
+    HIP_TRY(launch_relayout_variant(c->hd, c->variant, c->ptrs, c->plan.tiles, c->stream), "relayout launch");
   HIP_TRY(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
   return FNNUE_OK;
 }
@@ -293,6 +303,42 @@ int fnnue_net_load_mem(const void* buf, size_t len, fnnue_net** out) {
   return FNNUE_OK;
 }
 
+int fnnue_net_load_variant_mem(const void* buf, size_t len, int variant, fnnue_net** out) {
+  if (!buf || !out) return fail(FNNUE_E_ARG, "null argument");
+  *out = nullptr;
+  if (variant != FNNUE_VARIANT_CRAZYHOUSE && variant != FNNUE_VARIANT_ATOMIC)
+    return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  std::unique_ptr<fnnue_net> n(new (std::nothrow) fnnue_net);
+  if (!n) return fail(FNNUE_E_OOM, "host allocation failed");
+  std::string err;
+  try {
+    const int rc = parse_net(static_cast<const uint8_t*>(buf), len, n->net, err, variant);
+    if (rc) return fail(rc, err);
+  } catch (const std::bad_alloc&) {
+    return fail(FNNUE_E_OOM, "host allocation failed");
+  }
+  *out = n.release();
+  return FNNUE_OK;
+}
+
+int fnnue_net_load_variant(const char* path, int variant, fnnue_net** out) {
+  if (!path || !out) return fail(FNNUE_E_ARG, "null argument");
+  *out = nullptr;
+  std::ifstream f(path, std::ios::binary | std::ios::ate);
+  if (!f) return fail(FNNUE_E_IO, std::string("cannot open ") + path);
+  const std::streamsize len = f.tellg();
+  f.seekg(0);
+  std::vector<uint8_t> buf((size_t)len);
+  if (!f.read(reinterpret_cast<char*>(buf.data()), len)) return fail(FNNUE_E_IO, std::string("cannot read ") + path);
+  return fnnue_net_load_variant_mem(buf.data(), buf.size(), variant, out);
+}
+
+int fnnue_net_variant(const fnnue_net* net, int* variant) {
+  if (!net || !variant) return fail(FNNUE_E_ARG, "null argument");
+  *variant = net->net.variant;
+  return FNNUE_OK;
+}
+
 int fnnue_net_load(const char* path, fnnue_net** out) {
   if (!path || !out) return fail(FNNUE_E_ARG, "null argument");
   *out = nullptr;
@@ -334,6 +380,27 @@ int fnnue_net_synthesize(uint64_t seed, uint32_t hd, uint32_t flags, void** buf,
   return FNNUE_OK;
 }
 
+int fnnue_net_synthesize_variant(uint64_t seed, uint32_t hd, int variant, uint32_t flags, void** buf, size_t* len) {
+  if (!buf || !len) return fail(FNNUE_E_ARG, "null argument");
+  if (variant != FNNUE_VARIANT_CRAZYHOUSE && variant != FNNUE_VARIANT_ATOMIC)
+    return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  if (!hd_supported(hd)) return fail(FNNUE_E_ARCH, "unsupported hd");
+  try {
+    Net n;
+    synthesize_net(seed, hd, flags, n, variant);
+    std::vector<uint8_t> bytes;
+    write_net(n, flags & FNNUE_SYNTH_LEB128, bytes);
+    void* p = std::malloc(bytes.size());
+    if (!p) return fail(FNNUE_E_OOM, "host allocation failed");
+    std::memcpy(p, bytes.data(), bytes.size());
+    *buf = p;
+    *len = bytes.size();
+  } catch (const std::bad_alloc&) {
+    return fail(FNNUE_E_OOM, "host allocation failed");
+  }
+  return FNNUE_OK;
+}
+
 void fnnue_buffer_free(void* buf) { std::free(buf); }
 
 int fnnue_device_count(int* count) {
@@ -346,13 +413,13 @@ int fnnue_device_count(int* count) {
 
 int fnnue_net_image_size(const fnnue_net* net, size_t* bytes) {
   if (!net || !bytes) return fail(FNNUE_E_ARG, "null argument");
-  *bytes = image_layout(net->net.hd).total;
+  *bytes = image_layout(net->net.hd, net->net.nfeat).total;
   return FNNUE_OK;
 }
 
 int fnnue_net_image_pack(const fnnue_net* net, void* host_buf, size_t bytes) {
   if (!net || !host_buf) return fail(FNNUE_E_ARG, "null argument");
-  if (bytes < image_layout(net->net.hd).total) return fail(FNNUE_E_CAPACITY, "image buffer too small");
+  if (bytes < image_layout(net->net.hd, net->net.nfeat).total) return fail(FNNUE_E_CAPACITY, "image buffer too small");
   pack_image(net->net, static_cast<uint8_t*>(host_buf));
   return FNNUE_OK;
 }
@@ -360,7 +427,7 @@ int fnnue_net_image_pack(const fnnue_net* net, void* host_buf, size_t bytes) {
 int fnnue_ctx_create(const fnnue_net* net, int device, fnnue_ctx** out) {
   if (!net || !out) return fail(FNNUE_E_ARG, "null argument");
   fnnue_ctx* c = nullptr;
-  int rc = ctx_alloc(device, net->net.hd, &c);
+  int rc = ctx_alloc(device, net->net.hd, &c, net->net.variant);
   if (rc) return rc;
   std::vector<uint8_t> img;
   try {
@@ -389,7 +456,7 @@ int fnnue_ctx_create_from_image(int device, uint32_t hd, const void* device_imag
   if (!hd_supported(hd)) return fail(FNNUE_E_ARCH, "unsupported hd");
   if (bytes != image_layout(hd).total) return fail(FNNUE_E_ARG, "image size does not match hd");
   fnnue_ctx* c = nullptr;
-  int rc = ctx_alloc(device, hd, &c);
+  int rc = ctx_alloc(device, hd, &c, kVariantChess);
   if (rc) return rc;
   DeviceGuard g(device);
   hipError_t e = hipMemcpy(c->image, device_image, bytes, hipMemcpyDeviceToDevice);
@@ -480,6 +547,7 @@ int fnnue_ctx_timing_read(fnnue_ctx* ctx, uint32_t* launches, double* ft_ms, dou
 int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n, int32_t* d_psqt,
                                 int32_t* d_positional, void* stream) {
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant != kVariantChess) return fail(FNNUE_E_ARCH, "variant net: use fnnue_eval_vpositions*");
   if (n == 0) return FNNUE_OK;
   if (!d_pos || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
   DeviceGuard g(ctx->device);
@@ -516,6 +584,7 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
   // d_off is device memory; the chunking needs the group boundaries on the
   // host, so this entry point copies them once (ngroups+1 words).
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant != kVariantChess) return fail(FNNUE_E_ARCH, "variant net: use fnnue_eval_vgroups*");
   if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
   if (ngroups == 0) return FNNUE_OK;
   if (!d_pos || !d_off || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
@@ -569,6 +638,56 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
     }
     if (rc) return rc;
     gb = ge;
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_eval_vpositions_device(fnnue_ctx* ctx, const fnnue_vpos* d_pos, size_t n, int32_t* d_psqt,
+                                 int32_t* d_positional, void* stream) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant == kVariantChess) return fail(FNNUE_E_ARCH, "chess net: use fnnue_eval_positions*");
+  if (n == 0) return FNNUE_OK;
+  if (!d_pos || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  int rc = order_workspace(ctx, s);
+  if (rc) return rc;
+  for (size_t b = 0; b < n; b += ctx->chunk) {
+    const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
+    std::array<hipEvent_t, 4>* ev = nullptr;
+    if ((rc = next_events(ctx, &ev))) return rc;
+    if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+    HIP_TRY(launch_variant_plan(d_pos + b, m, ctx->variant, ctx->plan, d_psqt + b, ctx->bucket, ctx->err, s),
+            "variant plan launch");
+    if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
+    HIP_TRY(launch_variant_ft(ctx->hd, ctx->variant, m, ctx->ptrs, ctx->plan, ctx->x, s), "variant ft launch");
+    if ((rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, ctx->plan.perm, ctx->plan.psqt_part, d_psqt + b)))
+      return rc;
+  }
+  return FNNUE_OK;
+}
+
+int fnnue_eval_vpositions(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t n, int32_t* psqt, int32_t* positional) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant == kVariantChess) return fail(FNNUE_E_ARCH, "chess net: use fnnue_eval_positions*");
+  if (n == 0) return FNNUE_OK;
+  if (!pos || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
+  DeviceGuard g(ctx->device);
+  const size_t step = std::min<size_t>(n, 4 * (size_t)ctx->chunk);
+  int rc = ensure_stage(ctx, step, 0);
+  if (rc) return rc;
+  fnnue_vpos* d_vpos = reinterpret_cast<fnnue_vpos*>(ctx->d_pos);  // staging sized for fnnue_vpos
+  for (size_t b = 0; b < n; b += step) {
+    const size_t m = std::min(step, n - b);
+    HIP_TRY(hipMemcpyAsync(d_vpos, pos + b, m * sizeof(fnnue_vpos), hipMemcpyHostToDevice, ctx->stream), "H2D");
+    rc = fnnue_eval_vpositions_device(ctx, d_vpos, m, ctx->d_psqt, ctx->d_positional, ctx->stream);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(psqt + b, ctx->d_psqt, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    HIP_TRY(hipMemcpyAsync(positional + b, ctx->d_positional, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if ((rc = latched(ctx)) == FNNUE_E_POSITION) return fail(rc, "invalid variant position in positions " +
+                                                               std::to_string(b) + ".." + std::to_string(b + m));
+    if (rc) return rc;
   }
   return FNNUE_OK;
 }

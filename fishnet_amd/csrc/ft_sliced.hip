@@ -181,7 +181,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
 // Items of a unit are sorted by piece count, so a pass's longest list is that
 // of its item 7 (clamped into the unit).  kSwar: the tile is converted to SWAR
 // words on its way into LDS and rows are summed as 32-bit words (swar_word).
-template <int HD, bool kSwar>
+template <int HD, bool kSwar, class G = ChessGeom>
 __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict__ tiles,
                                                          const int16_t* __restrict__ ftb,
                                                          const uint32_t* __restrict__ ctr,
@@ -192,14 +192,15 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
                                                          int32_t* __restrict__ psqt_part,
                                                          uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
+  constexpr int kTileU4 = G::kTileU4;
   __shared__ uint4 img[kTileU4];
-  __shared__ int32_t ptile[kTileRows * kPsqtBuckets];  // slice 0 only: PSQT rows of the king block
+  __shared__ int32_t ptile[G::kTileRows * kPsqtBuckets];  // slice 0 only: PSQT rows of the king block
   __shared__ uint2 lbuf[16][64];                       // per wave: one pass's 8 feature lists
   const uint32_t w = blockIdx.x;
   const uint32_t j = w >> 3;
   const uint32_t unit = (j / S) * 8 + (w & 7);
   const int s = (int)(j % S);
-  if (unit >= ctr[kNUnits]) return;
+  if (unit >= ctr[G::kNUnitsWord]) return;
   const int4 u = units[unit];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -209,7 +210,8 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   // store, and the first passes' lists behind them, so the fetch costs one
   // round trip instead of one per 16 KiB.
   constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
-  constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
+  constexpr int kPtileU4 = G::kTileRows * kPsqtBuckets / 4, kPtileRealU4 = G::kRows * kPsqtBuckets / 4;
+  static_assert(kPtileU4 <= 2048, "PSQT tile loads: two per thread");
   const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
   uint4 t[kTileLoads];
 #pragma unroll
@@ -220,15 +222,15 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
     t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
 #endif
   uint4 pt[2];
-  const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
+  const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * G::kRows * kPsqtBuckets);
   if (s == 0) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
   }
   u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
   u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
-  const int krow = king_row(u.x);
-  const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
+  const int krow = G::king_row(u.x);
+  const char* lbase = reinterpret_cast<const char*>(img) + G::kPlaneBytes * q;
   uint2* lb = lbuf[wv];
   const __amdgpu_buffer_rsrc_t psqt_rsrc = __builtin_amdgcn_make_buffer_rsrc(psqt_part, 0, kBufferRange, kBufferFlags);
   const __amdgpu_buffer_rsrc_t x_rsrc = __builtin_amdgcn_make_buffer_rsrc(x, 0, kBufferAll, kBufferFlags);
@@ -287,18 +289,24 @@ hipError_t relayout_t(const NetPtrs& net, void* tiles, hipStream_t stream) {
   return hipGetLastError();
 }
 
-template <int HD>
+template <int HD, class G = ChessGeom>
 hipError_t ft_slices_t(const SlicedPlan& P, const NetPtrs& net, uint8_t* x, uint32_t max_units, hipStream_t stream) {
   constexpr int S = HD / 64;
   const uint32_t groups = (max_units + 7) / 8;
   if (P.swar)
-    hipLaunchKernelGGL((ft_slices_kernel<HD, true>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+    hipLaunchKernelGGL((ft_slices_kernel<HD, true, G>), dim3(groups * 8 * S), dim3(1024), 0, stream,
                        (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
                        P.psqt_part, x);
   else
-    hipLaunchKernelGGL((ft_slices_kernel<HD, false>), dim3(groups * 8 * S), dim3(1024), 0, stream,
+    hipLaunchKernelGGL((ft_slices_kernel<HD, false, G>), dim3(groups * 8 * S), dim3(1024), 0, stream,
                        (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, P.items, P.flist, net.psqt_w,
                        P.psqt_part, x);
+  return hipGetLastError();
+}
+
+template <int HD, class G>
+hipError_t relayout_g(const NetPtrs& net, void* tiles, hipStream_t stream) {
+  hipLaunchKernelGGL((relayout_kernel<HD, G>), dim3(2048), dim3(256), 0, stream, net.ft_w, (uint4*)tiles);
   return hipGetLastError();
 }
 
@@ -352,6 +360,46 @@ hipError_t launch_sliced_ft(uint32_t hd, uint32_t n, const NetPtrs& net, const S
 #define CALL(H) ft_slices_t<H>(P, net, x, mu, stream)
   FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
+}
+
+// ---- Fairy-Stockfish variant feature sets on the same kernel (variant.hip plans) ----
+size_t variant_tiles_bytes(uint32_t hd, int variant) {
+  const int planes = variant == kVariantCrazyhouse ? VariantGeom<kVBoardRows + kVHandRows>::kTileU4
+                                                   : VariantGeom<kVBoardRows>::kTileU4;
+  return (size_t)64 * (hd / 64) * planes * sizeof(uint4);
+}
+
+// Variant nets come in widths 256 / 512 / 1024 (kernels_support_variant).
+#define FNNUE_VHD_DISPATCH(hd, CALL)      \
+  switch (hd) {                           \
+    case 256: return CALL(256);           \
+    case 512: return CALL(512);           \
+    case 1024: return CALL(1024);         \
+    default: return hipErrorInvalidValue; \
+  }
+#define FNNUE_VARIANT_DISPATCH(variant, CALLG)                                   \
+  if (variant == kVariantCrazyhouse) {                                          \
+    using G = VariantGeom<kVBoardRows + kVHandRows>;                            \
+    FNNUE_VHD_DISPATCH(hd, CALLG)                                               \
+  } else if (variant == kVariantAtomic) {                                       \
+    using G = VariantGeom<kVBoardRows>;                                         \
+    FNNUE_VHD_DISPATCH(hd, CALLG)                                               \
+  }                                                                             \
+  return hipErrorInvalidValue;
+
+hipError_t launch_relayout_variant(uint32_t hd, int variant, const NetPtrs& net, void* tiles, hipStream_t stream) {
+#define CALLG(H) relayout_g<H, G>(net, tiles, stream)
+  FNNUE_VARIANT_DISPATCH(variant, CALLG)
+#undef CALLG
+}
+
+hipError_t launch_variant_ft(uint32_t hd, int variant, uint32_t n, const NetPtrs& net, const SlicedPlan& P, uint8_t* x,
+                             hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint32_t mu = variant_max_units(n);
+#define CALLG(H) ft_slices_t<H, G>(P, net, x, mu, stream)
+  FNNUE_VARIANT_DISPATCH(variant, CALLG)
+#undef CALLG
 }
 
 hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const NetPtrs& net, const SlicedPlan& P,

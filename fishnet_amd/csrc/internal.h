@@ -19,6 +19,8 @@ struct fnnue_net {
 struct fnnue_ctx {
   int device = 0;
   uint32_t hd = 0;
+  int variant = 0;             // fnnue::kVariant* of the net (chess or a Fairy-Stockfish feature set)
+  uint32_t nfeat = 0;          // feature rows of the net
   uint8_t* image = nullptr;
   size_t image_bytes = 0;
   fnnue::NetPtrs ptrs{};
@@ -75,7 +77,7 @@ struct DeviceGuard {
 
 void ctx_destroy(fnnue_ctx* c);
 // Allocates a context on `device` for width hd: everything except the image contents.
-int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out);
+int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant);
 // Derives the LDS-tile layout of the FT weights from the (just written) image.
 int finish_upload(fnnue_ctx* c);
 // Reads and clears the latched device error word.

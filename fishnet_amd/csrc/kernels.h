@@ -70,6 +70,19 @@ hipError_t launch_ft_sliced(uint32_t hd, const fnnue_pos* pos, uint32_t n, const
                             uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err, hipStream_t stream,
                             hipEvent_t mid = nullptr);
 
+// Fairy-Stockfish variant nets (net.h kVariant*): positions fnnue_vpos; the
+// plan (variant.hip) fills a SlicedPlan with the variant counter layout, the
+// main kernel is ft_slices over the variant tile geometry, then launch_stack
+// with P.perm / P.psqt_part as for chess.
+size_t variant_tiles_bytes(uint32_t hd, int variant);
+uint32_t variant_max_units(uint32_t chunk);
+size_t variant_ctr_words();
+hipError_t launch_relayout_variant(uint32_t hd, int variant, const NetPtrs& net, void* tiles, hipStream_t stream);
+hipError_t launch_variant_plan(const fnnue_vpos* pos, uint32_t n, int variant, const SlicedPlan& P, int32_t* psqt,
+                               uint8_t* bucket, uint32_t* err, hipStream_t stream);
+hipError_t launch_variant_ft(uint32_t hd, int variant, uint32_t n, const NetPtrs& net, const SlicedPlan& P, uint8_t* x,
+                             hipStream_t stream);
+
 // Incremental FT on LDS tiles for CHAIN / STAR groups (ft_segments.hip).
 // Uses the sliced plan's tiles, counters, unit table, lists and psqt_part;
 // writes x[i], bucket[i], psqt_part[2i + half] in position order, then run

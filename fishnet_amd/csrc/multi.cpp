@@ -114,7 +114,7 @@ int fnnue_multi_create(const fnnue_net* net, const int* devices, int ndev, fnnue
   m->ctx.assign(ndev, nullptr);
   const uint32_t hd = net->net.hd;
   for (int i = 0; i < ndev; ++i)
-    if (int rc = ctx_alloc(devices[i], hd, &m->ctx[i])) return rc;
+    if (int rc = ctx_alloc(devices[i], hd, &m->ctx[i], net->net.variant)) return rc;
   // net image: packed once on the host, uploaded to devices[0] ...
   std::vector<uint8_t> img;
   try {

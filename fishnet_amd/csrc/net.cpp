@@ -22,7 +22,9 @@ static uint32_t affine_hash(uint32_t prev, uint32_t out) {
 // layers/clipped_relu.h get_hash_value
 static uint32_t crelu_hash(uint32_t prev) { return 0x538D24C7u + prev; }
 
-uint32_t ft_hash(uint32_t hd) { return kFtHashBase ^ (hd * 2); }
+uint32_t ft_hash(uint32_t hd, int variant) {
+  return (variant == kVariantChess ? kFtHashBase : kFtHashBaseVariants) ^ (hd * 2);
+}
 
 uint32_t net_hash(uint32_t hd) {
   uint32_t h = kNetHashBase ^ (hd * 2);
@@ -111,7 +113,7 @@ struct Writer {
 
 }  // namespace
 
-int parse_net(const uint8_t* buf, size_t len, Net& net, std::string& err) {
+int parse_net(const uint8_t* buf, size_t len, Net& net, std::string& err, int variant) {
   Reader r{buf, len};
   const uint32_t version = r.u32(), file_hash = r.u32(), dlen = r.u32();
   if (r.fail) { err = "truncated header"; return FNNUE_E_FORMAT; }
@@ -120,15 +122,24 @@ int parse_net(const uint8_t* buf, size_t len, Net& net, std::string& err) {
   net.desc.assign((const char*)buf + r.off, dlen);
   r.off += dlen;
   const uint32_t fth = r.u32();
-  const uint32_t hd = (fth ^ kFtHashBase) / 2;
-  if (r.fail || ft_hash(hd) != fth) { err = "feature transformer hash is not HalfKAv2_hm"; return FNNUE_E_FORMAT; }
+  const uint32_t hd = (fth ^ ft_hash(0, variant)) / 2;
+  if (r.fail || ft_hash(hd, variant) != fth) {
+    err = variant == kVariantChess ? "feature transformer hash is not HalfKAv2_hm"
+                                   : "feature transformer hash is not HalfKAv2 (variants)";
+    return FNNUE_E_FORMAT;
+  }
   if (!hd_supported(hd)) { err = "unsupported transformed feature dimension " + std::to_string(hd); return FNNUE_E_ARCH; }
-  if ((ft_hash(hd) ^ net_hash(hd)) != file_hash) { err = "file hash does not match the SFNNv5 structure"; return FNNUE_E_FORMAT; }
+  if ((ft_hash(hd, variant) ^ net_hash(hd)) != file_hash) {
+    err = "file hash does not match the SFNNv5 structure";
+    return FNNUE_E_FORMAT;
+  }
+  net.variant = variant;
+  net.nfeat = features_of(variant);
   net.hd = hd;
   net.file_hash = file_hash;
   net.ft_bias.resize(hd);
-  net.ft_w.resize((size_t)hd * kFeatures);
-  net.psqt_w.resize((size_t)kPsqtBuckets * kFeatures);
+  net.ft_w.resize((size_t)hd * net.nfeat);
+  net.psqt_w.resize((size_t)kPsqtBuckets * net.nfeat);
   r.ints(net.ft_bias.data(), hd);
   r.ints(net.ft_w.data(), net.ft_w.size());
   r.ints(net.psqt_w.data(), net.psqt_w.size());
@@ -154,10 +165,10 @@ void write_net(const Net& net, bool leb, std::vector<uint8_t>& out) {
   out.clear();
   Writer w{out};
   w.u32(kVersion);
-  w.u32(ft_hash(net.hd) ^ net_hash(net.hd));
+  w.u32(ft_hash(net.hd, net.variant) ^ net_hash(net.hd));
   w.u32((uint32_t)net.desc.size());
   out.insert(out.end(), net.desc.begin(), net.desc.end());
-  w.u32(ft_hash(net.hd));
+  w.u32(ft_hash(net.hd, net.variant));
   w.ints(net.ft_bias.data(), net.ft_bias.size(), leb);
   w.ints(net.ft_w.data(), net.ft_w.size(), leb);
   w.ints(net.psqt_w.data(), net.psqt_w.size(), leb);
@@ -190,15 +201,18 @@ T clampT(double v, double lo, double hi) { return (T)std::llround(v < lo ? lo : 
 // Magnitudes are chosen so that every clamp regime of the evaluation is hit
 // (accumulators below 0, inside [0,127] and above 127; L1 outputs that
 // saturate CReLU and SqrCReLU both ways), see tests/test_oracle.py.
-void synthesize_net(uint64_t seed, uint32_t hd, uint32_t flags, Net& net) {
-  Rng g{seed * 0x2545F4914F6CDD1Dull + hd};
+void synthesize_net(uint64_t seed, uint32_t hd, uint32_t flags, Net& net, int variant) {
+  Rng g{seed * 0x2545F4914F6CDD1Dull + hd + 0x9E3779B97F4A7C15ull * (uint64_t)variant};
+  net.variant = variant;
+  net.nfeat = features_of(variant);
   net.hd = hd;
-  net.file_hash = ft_hash(hd) ^ net_hash(hd);
+  net.file_hash = ft_hash(hd, variant) ^ net_hash(hd);
   net.desc = "fishnet-amd synthetic SFNNv5 net seed=" + std::to_string(seed) + " hd=" + std::to_string(hd) +
-             " flags=" + std::to_string(flags);
+             " flags=" + std::to_string(flags) +
+             (variant ? " variant=" + std::string(variant == kVariantCrazyhouse ? "crazyhouse" : "atomic") : "");
   net.ft_bias.resize(hd);
-  net.ft_w.resize((size_t)hd * kFeatures);
-  net.psqt_w.resize((size_t)kPsqtBuckets * kFeatures);
+  net.ft_w.resize((size_t)hd * net.nfeat);
+  net.psqt_w.resize((size_t)kPsqtBuckets * net.nfeat);
   const bool wrap = flags & FNNUE_SYNTH_WRAP;
   for (auto& b : net.ft_bias) b = (int16_t)g.range(-16, 112);
   const double ftsd = wrap ? 9000.0 : 11.0;
@@ -226,12 +240,12 @@ void synthesize_net(uint64_t seed, uint32_t hd, uint32_t flags, Net& net) {
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-ImageLayout image_layout(uint32_t hd) {
+ImageLayout image_layout(uint32_t hd, uint32_t nfeat) {
   ImageLayout L{};
   size_t o = 0;
-  L.ft_w = o;    o = align256(o + (size_t)(kFeatures + 1) * hd * sizeof(int16_t));
+  L.ft_w = o;    o = align256(o + (size_t)(nfeat + 1) * hd * sizeof(int16_t));
   L.ft_bias = o; o = align256(o + (size_t)hd * sizeof(int16_t));
-  L.psqt_w = o;  o = align256(o + (size_t)(kFeatures + 1) * kPsqtBuckets * sizeof(int32_t));
+  L.psqt_w = o;  o = align256(o + (size_t)(nfeat + 1) * kPsqtBuckets * sizeof(int32_t));
   L.w0 = o;      o = align256(o + (size_t)kStacks * kL2 * hd);
   L.b0 = o;      o = align256(o + (size_t)kStacks * kL2 * sizeof(int32_t));
   L.w1 = o;      o = align256(o + (size_t)kStacks * kL3 * kFc1In);
@@ -244,7 +258,7 @@ ImageLayout image_layout(uint32_t hd) {
 
 void pack_image(const Net& net, uint8_t* dst) {
   const uint32_t hd = net.hd;
-  const ImageLayout L = image_layout(hd);
+  const ImageLayout L = image_layout(hd, net.nfeat);
   std::memset(dst, 0, L.total);
   std::memcpy(dst + L.ft_w, net.ft_w.data(), net.ft_w.size() * sizeof(int16_t));
   std::memcpy(dst + L.ft_bias, net.ft_bias.data(), hd * sizeof(int16_t));
@@ -260,15 +274,17 @@ void pack_image(const Net& net, uint8_t* dst) {
   }
 }
 
-int32_t accumulator_bound(const int16_t* ft_w, const int16_t* ft_bias, uint32_t hd) {
-  constexpr int kRows = kFeatures / 32;  // rows per king block (704)
+int32_t accumulator_bound(const int16_t* ft_w, const int16_t* ft_bias, uint32_t hd, int variant) {
+  const int kRows = (int)(variant == kVariantChess ? kFeatures / 32 : variant_rows(variant));  // rows per king block
+  const int kBlocks = variant == kVariantChess ? 32 : 64;
   const uint32_t ncol = hd / 2;          // even columns
   int64_t worst = 0;
   std::vector<int32_t> mag((size_t)ncol * kRows);  // [even column][row], |w|
-  for (int kb = 0; kb < 32; ++kb) {
+  for (int kb = 0; kb < kBlocks; ++kb) {
     // own-king row of king block kb: plane 10, oriented king square on files e-h
-    // (KingBuckets is a bijection kb <-> oriented square; upstream half_ka_v2_hm.h)
-    const int krow = 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3));
+    // (KingBuckets is a bijection kb <-> oriented square; upstream half_ka_v2_hm.h);
+    // variants: block kb = oriented king square itself
+    const int krow = variant == kVariantChess ? 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3)) : 640 + kb;
     const int16_t* blk = ft_w + (size_t)kb * kRows * hd;
     for (int r = 0; r < kRows; ++r)
       for (uint32_t c = 0; c < ncol; ++c)

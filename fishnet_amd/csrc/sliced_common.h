@@ -21,6 +21,7 @@ constexpr int kNoRow = kRowsPerBlock;         // the zero row
 // conflict-free and rows of opposite parity use complementary banks.
 constexpr int kPlaneBytes = 11296;
 constexpr int kPlaneU4 = kPlaneBytes / 16;    // 706
+constexpr int kPlaneU4_ = kPlaneU4;
 constexpr int kTileU4 = 8 * kPlaneU4;         // 5648 x 16 B = 90,368 B
 // Feature-list entries are 16*row (u16), the byte offset of the row inside a
 // plane: ft_slices forms the LDS address base_q + entry with one SDWA add.
@@ -39,6 +40,31 @@ constexpr int kScatterPositions = PLAN_WG;    // positions per plan_scatter work
 
 // Counter block layout (uint32 words).
 constexpr int kCnt = 0, kOff = kBins, kCur = 2 * kBins, kNUnits = 3 * kBins;
+
+// Tile geometry of a feature set, for ft_slices / relayout:
+//   kRows      feature rows per own-king block (the rows a tile holds)
+//   kPlaneU4   16-B entries per plane: rows + zero rows, kPlaneU4 * 16 = 32
+//              (mod 256) so rows of opposite parity use complementary banks
+//   kBlocks    own-king blocks; king_row(kb) = the own king's row in block
+//              kb (the same for every item of kb: folded into the bias)
+//   kNUnitsWord  counter word holding the unit count (plan layout)
+struct ChessGeom {  // HalfKAv2_hm: 32 mirrored king buckets x 704 rows
+  static constexpr int kRows = kRowsPerBlock, kPlaneU4 = kPlaneU4_, kBlocks = 32, kNUnitsWord = kNUnits;
+  static constexpr int kTileRows = kRows + 1, kPlaneBytes = 16 * kPlaneU4, kTileU4 = 8 * kPlaneU4;
+  __host__ __device__ static constexpr int king_row(int kb) { return fnnue::king_row(kb); }
+};
+// Fairy-Stockfish HalfKAv2 variants (net.h): 64 king squares x R rows, own
+// king row 640 + oriented king square (= kb).  Counters: kVBins bins of
+// (kb, list length) and 9 position bins, laid out as the chess block.
+constexpr int kVItemBins = 64 * 33, kVBins = kVItemBins + kPosBins;
+constexpr int kVCnt = 0, kVOff = kVBins, kVCur = 2 * kVBins, kVNUnits = 3 * kVBins;
+template <int R>
+struct VariantGeom {
+  static_assert(R % 16 == 0, "plane stride must stay 32 mod 256");
+  static constexpr int kRows = R, kPlaneU4 = R + 2, kBlocks = 64, kNUnitsWord = kVNUnits;
+  static constexpr int kTileRows = kRows + 1, kPlaneBytes = 16 * kPlaneU4, kTileU4 = 8 * kPlaneU4;
+  __host__ __device__ static constexpr int king_row(int kb) { return 640 + kb; }
+};
 
 // ds_read_b128 services a wave in four 16-lane groups {0-3,12-15,20-27},
 // {4-11,16-19,28-31} (+32).  Give each group exactly two items of 8 lanes so
@@ -130,7 +156,7 @@ __host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
 
 // One workgroup of 1024 threads.  unit_items = 0: segment units (see
 // kSegUnitPlies) instead of fixed-size ones.
-__global__ __launch_bounds__(1024) void plan_scan_kernel(uint32_t* __restrict__ ctr, int4* __restrict__ units,
+__global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel(uint32_t* __restrict__ ctr, int4* __restrict__ units,
                                                          uint32_t unit_items) {
   __shared__ uint32_t s[kBins];
   __shared__ uint32_t part[1024];
@@ -281,21 +307,21 @@ __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ks
 __host__ __device__ constexpr size_t tile_uint4_count(uint32_t hd) { return (size_t)32 * (hd / 64) * kTileU4; }
 
 // ---------------------------------------------------------------------------
-// Tile image: tile(kb, s)[q][r] (16 B) = {ft_w[kb*704+r][32s+4q .. +3],
-// ft_w[kb*704+r][HD/2+32s+4q .. +3]}; r = 704 is the zero row, r = 705 padding.
-template <int HD>
+// Tile image: tile(kb, s)[q][r] (16 B) = {ft_w[kb*R+r][32s+4q .. +3],
+// ft_w[kb*R+r][HD/2+32s+4q .. +3]}; rows r >= R (the zero rows) are zero.
+template <int HD, class G = ChessGeom>
 __global__ __launch_bounds__(256) void relayout_kernel(const int16_t* __restrict__ ftw, uint4* __restrict__ tiles) {
   constexpr int S = HD / 64;
-  constexpr size_t total = tile_uint4_count(HD);
+  constexpr size_t total = (size_t)G::kBlocks * S * G::kTileU4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int r = (int)(i % kPlaneU4);
-    const size_t t = i / kPlaneU4;
+    const int r = (int)(i % G::kPlaneU4);
+    const size_t t = i / G::kPlaneU4;
     const int q = (int)(t & 7);
     const size_t ks = t >> 3;
     const int s = (int)(ks % S), kb = (int)(ks / S);
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < kRowsPerBlock) {
-      const int16_t* row = ftw + (size_t)(kb * kRowsPerBlock + r) * HD;
+    if (r < G::kRows) {
+      const int16_t* row = ftw + (size_t)(kb * G::kRows + r) * HD;
       const uint2 lo = *reinterpret_cast<const uint2*>(row + 32 * s + 4 * q);
       const uint2 hi = *reinterpret_cast<const uint2*>(row + HD / 2 + 32 * s + 4 * q);
       v = make_uint4(lo.x, lo.y, hi.x, hi.y);

@@ -38,6 +38,26 @@ class Net:
         return cls(h.value)
 
     @classmethod
+    def load_variant(cls, path: str, variant: int) -> "Net":
+        """A Fairy-Stockfish variant net (VARIANT_CRAZYHOUSE / VARIANT_ATOMIC)."""
+        h = C.c_void_p()
+        N.check(N.lib.fnnue_net_load_variant(path.encode(), variant, C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_bytes_variant(cls, data: bytes, variant: int) -> "Net":
+        h = C.c_void_p()
+        buf = C.create_string_buffer(data, len(data))
+        N.check(N.lib.fnnue_net_load_variant_mem(buf, len(data), variant, C.byref(h)))
+        return cls(h.value)
+
+    @property
+    def variant(self) -> int:
+        v = C.c_int()
+        N.check(N.lib.fnnue_net_variant(self._h, C.byref(v)))
+        return v.value
+
+    @classmethod
     def from_bytes(cls, data: bytes) -> "Net":
         h = C.c_void_p()
         buf = C.create_string_buffer(data, len(data))
@@ -82,6 +102,36 @@ def synthesize_net(seed: int, hd: int = 1024, flags: int = 0) -> bytes:
         return C.string_at(buf.value, size.value)
     finally:
         N.lib.fnnue_buffer_free(buf)
+
+
+def synthesize_variant_net(seed: int, hd: int, variant: int, flags: int = 0) -> bytes:
+    """Deterministic synthetic Fairy-Stockfish variant net in the .nnue format."""
+    buf, size = C.c_void_p(), C.c_size_t()
+    N.check(N.lib.fnnue_net_synthesize_variant(seed, hd, variant, flags, C.byref(buf), C.byref(size)))
+    try:
+        return C.string_at(buf.value, size.value)
+    finally:
+        N.lib.fnnue_buffer_free(buf)
+
+
+def vpos_from_fen(variant: int, fen: str) -> np.ndarray:
+    out = N.vpositions_array(1)
+    N.check(N.lib.fnnue_vpos_from_fen(variant, fen.encode(), N.ptr(out)))
+    return out[0]
+
+
+def random_vpositions(seed: int, variant: int, count: int, max_plies: int = 120, mode: int = N.PLAYOUT_FINAL):
+    """Seeded pseudo-legal random walks of a variant (test inputs).  FINAL ->
+    positions; PLIES -> (positions, CHAIN group offsets)."""
+    cap = count if mode == N.PLAYOUT_FINAL else count * (max_plies + 1)
+    out = N.vpositions_array(cap)
+    off = np.zeros(count + 1, dtype=np.uint32)
+    n, g = C.c_size_t(), C.c_size_t()
+    N.check(N.lib.fnnue_random_vpositions(seed, variant, count, max_plies, mode, N.ptr(out), cap, N.ptr(off), len(off),
+                                          C.byref(n), C.byref(g)))
+    if mode == N.PLAYOUT_FINAL:
+        return out[: n.value]
+    return out[: n.value], off[: g.value + 1]
 
 
 def device_count() -> int:
@@ -133,6 +183,19 @@ class Evaluator:
         N.check(N.lib.fnnue_eval_groups(self._h, N.ptr(pos), n, N.ptr(off), len(off) - 1, mode,
                                         N.ptr(psqt), N.ptr(positional)))
         return psqt, positional
+
+    def eval_vpositions(self, vpos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """Fairy-Stockfish variant positions (fnnue_vpos, 48 B) on a variant-net context."""
+        vpos = np.ascontiguousarray(vpos, dtype=np.uint8).reshape(-1, N.VPOS_BYTES)
+        n = vpos.shape[0]
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_eval_vpositions(self._h, N.ptr(vpos), n, N.ptr(psqt), N.ptr(positional)))
+        return psqt, positional
+
+    def eval_vpositions_device(self, d_pos: int, n: int, d_psqt: int, d_positional: int, stream: int | None):
+        N.check(N.lib.fnnue_eval_vpositions_device(self._h, C.c_void_p(d_pos), n, C.c_void_p(d_psqt),
+                                                   C.c_void_p(d_positional), C.c_void_p(stream)))
 
     # Device-pointer entry points (inputs resident in HBM; asynchronous).
     def eval_positions_device(self, d_pos: int, n: int, d_psqt: int, d_positional: int, stream: int | None):

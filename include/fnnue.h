@@ -65,6 +65,17 @@ typedef struct {
   uint8_t pad[3];
 } fnnue_pos;
 
+/* Packed position of a Fairy-Stockfish variant (48 bytes): the board and side
+ * to move as fnnue_pos, then the pieces in hand (crazyhouse pockets): hand[0..4]
+ * = white P N B R Q, hand[5..9] = black P N B R Q, each <= 16; all zero for
+ * variants without pockets. */
+typedef struct {
+  uint8_t sq[32];
+  uint8_t stm;
+  uint8_t hand[10];
+  uint8_t pad[5];
+} fnnue_vpos;
+
 /* ---- errors ---- */
 const char *fnnue_last_error(void);
 /* ABI version: (major << 16) | minor. */
@@ -90,6 +101,39 @@ void fnnue_net_free(fnnue_net *net);
 #define FNNUE_SYNTH_FC1_PAD 4u    /* non-zero fc_1 padding weights (inputs 30,31)      */
 int fnnue_net_synthesize(uint64_t seed, uint32_t hd, uint32_t flags, void **buf, size_t *len);
 void fnnue_buffer_free(void *buf);
+
+/* ---- Fairy-Stockfish variant nets (BASELINE config 5) ----
+ * The reference routes every variant to Fairy-Stockfish ([ref]
+ * src/queue.rs:530-539, src/assets.rs:384-391) and runs it with its classical
+ * eval (`Use NNUE false`, src/stockfish.rs:248-260); these entry points are the
+ * NNUE evaluation of such positions with Fairy-Stockfish's variant feature set
+ * ("HalfKAv2 variants", 8x8 boards, 64 own-king squares, no mirroring; pocket
+ * features for crazyhouse) in front of the SF 15.1 layer stacks.  Recalled,
+ * not read: parity unpinned.  Same file format; the feature
+ * transformer hash is 0x5F234CB8 ^ 2*HD; widths 256, 512, 1024. */
+#define FNNUE_VARIANT_CHESS 0
+#define FNNUE_VARIANT_CRAZYHOUSE 1 /* 64 x (704 board + 160 hand) features */
+#define FNNUE_VARIANT_ATOMIC 2     /* 64 x 704 board features (also kingofthehill, racingkings) */
+int fnnue_net_load_variant(const char *path, int variant, fnnue_net **out);
+int fnnue_net_load_variant_mem(const void *buf, size_t len, int variant, fnnue_net **out);
+int fnnue_net_variant(const fnnue_net *net, int *variant);
+int fnnue_net_synthesize_variant(uint64_t seed, uint32_t hd, int variant, uint32_t flags, void **buf, size_t *len);
+/* FEN (crazyhouse holdings as "[PNbq]" after the placement or as a 9th
+ * placement field; "~" promotion marks ignored) -> packed variant position. */
+int fnnue_vpos_from_fen(int variant, const char *fen, fnnue_vpos *out);
+/* Test inputs: `count` seeded pseudo-legal random walks from the start
+ * position (captures go to the capturer's hand and drops come back out for
+ * crazyhouse; captures explode for atomic, kings never removed), up to
+ * max_plies each.  FNNUE_PLAYOUT_FINAL: the last position of each walk;
+ * FNNUE_PLAYOUT_PLIES: every position as CHAIN groups (off[], n_groups + 1). */
+int fnnue_random_vpositions(uint64_t seed, int variant, size_t count, uint32_t max_plies, int mode, fnnue_vpos *out,
+                            size_t cap, uint32_t *off, size_t off_cap, size_t *n_out, size_t *n_groups);
+/* Evaluation of variant positions on a context created from a variant net
+ * (fnnue_ctx_create / fnnue_multi_create): the LDS-stationary feature
+ * transformer over the variant tiles, then the MFMA layer stacks. */
+int fnnue_eval_vpositions(fnnue_ctx *ctx, const fnnue_vpos *pos, size_t n, int32_t *psqt, int32_t *positional);
+int fnnue_eval_vpositions_device(fnnue_ctx *ctx, const fnnue_vpos *d_pos, size_t n, int32_t *d_psqt,
+                                 int32_t *d_positional, void *stream);
 
 /* ---- device context ----
  * Replaces spawning + initialising an engine process ([ref] src/stockfish.rs:

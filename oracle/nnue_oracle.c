@@ -50,6 +50,9 @@ uint32_t oracle_net_hash(uint32_t hd) {
 
 /* nnue_feature_transformer.h: FeatureSet::HashValue ^ (OutputDimensions*2), OutputDimensions = HD */
 uint32_t oracle_ft_hash(uint32_t hd) { return O_FT_HASH_BASE ^ (hd * 2); }
+static uint32_t o_ft_hash_for(int variant, uint32_t hd) {
+    return (variant ? O_FT_HASH_BASE_VARIANTS : O_FT_HASH_BASE) ^ (hd * 2);
+}
 
 /* ---- little-endian stream (nnue_common.h read_little_endian / read_leb_128) ---- */
 typedef struct { const uint8_t *p; size_t n, off; int fail; } ostream;
@@ -115,7 +118,15 @@ void oracle_net_free(onet *n) {
  * Output x PaddedInput weights); must end exactly at EOF.
  * Returns 0 on success, negative code on failure. */
 int oracle_net_load_mem(const void *buf, size_t len, onet **out) {
+    return oracle_net_load_variant_mem(buf, len, 0, out);
+}
+
+/* The same file format for Fairy-Stockfish variant nets: only the feature
+ * set's hash and row count differ (variant 0 = chess HalfKAv2_hm). */
+int oracle_net_load_variant_mem(const void *buf, size_t len, int variant, onet **out) {
     *out = NULL;
+    const uint32_t nfeat = variant ? oracle_variant_features(variant) : O_FEATURES;
+    if (!nfeat) return -1;
     ostream s = { (const uint8_t *)buf, len, 0, 0 };
     uint32_t version = rd_u32(&s), file_hash = rd_u32(&s), dlen = rd_u32(&s);
     if (s.fail || version != O_VERSION) return -2;
@@ -125,18 +136,20 @@ int oracle_net_load_mem(const void *buf, size_t len, onet **out) {
     memcpy(n->desc, s.p + s.off, dlen); n->desc[dlen] = 0; s.off += dlen;
     n->file_hash = file_hash;
     uint32_t fth = rd_u32(&s);
-    uint32_t hd = (fth ^ O_FT_HASH_BASE) / 2;
-    if (s.fail || hd == 0 || hd > 4096 || (hd % 128) != 0 || oracle_ft_hash(hd) != fth) {
+    uint32_t hd = (fth ^ (variant ? O_FT_HASH_BASE_VARIANTS : O_FT_HASH_BASE)) / 2;
+    if (s.fail || hd == 0 || hd > 4096 || (hd % 128) != 0 || o_ft_hash_for(variant, hd) != fth) {
         oracle_net_free(n); return -4;
     }
     n->hd = hd;
-    if ((oracle_ft_hash(hd) ^ oracle_net_hash(hd)) != file_hash) { oracle_net_free(n); return -5; }
+    n->nfeat = nfeat;
+    n->variant = variant;
+    if ((o_ft_hash_for(variant, hd) ^ oracle_net_hash(hd)) != file_hash) { oracle_net_free(n); return -5; }
     n->ft_bias = (int16_t *)malloc(sizeof(int16_t) * hd);
-    n->ft_w = (int16_t *)malloc(sizeof(int16_t) * (size_t)hd * O_FEATURES);
-    n->psqt_w = (int32_t *)malloc(sizeof(int32_t) * (size_t)O_PSQT_BUCKETS * O_FEATURES);
+    n->ft_w = (int16_t *)malloc(sizeof(int16_t) * (size_t)hd * nfeat);
+    n->psqt_w = (int32_t *)malloc(sizeof(int32_t) * (size_t)O_PSQT_BUCKETS * nfeat);
     rd_ints(&s, 2, n->ft_bias, hd);
-    rd_ints(&s, 2, n->ft_w, (size_t)hd * O_FEATURES);
-    rd_ints(&s, 4, n->psqt_w, (size_t)O_PSQT_BUCKETS * O_FEATURES);
+    rd_ints(&s, 2, n->ft_w, (size_t)hd * nfeat);
+    rd_ints(&s, 4, n->psqt_w, (size_t)O_PSQT_BUCKETS * nfeat);
     if (s.fail) { oracle_net_free(n); return -6; }
     uint32_t nh = oracle_net_hash(hd);
     for (int b = 0; b < O_STACKS; ++b) {
@@ -253,12 +266,20 @@ int oracle_eval_board(const onet *n, const uint8_t *board, int stm, int32_t *psq
     int wk = -1, bk = -1;
     int cnt = o_check_board(board, &wk, &bk);
     if (cnt < 0 || (stm != 0 && stm != 1)) return -1;
-    const uint32_t hd = n->hd;
     int16_t acc[2][4096];
     int32_t psq[2][O_PSQT_BUCKETS];
+    if (n->variant) return -1;
     o_refresh(n, board, 0, wk, acc[0], psq[0]);
     o_refresh(n, board, 1, bk, acc[1], psq[1]);
-    const int bucket = (cnt - 1) / 4;
+    const int16_t *const a2[2] = { acc[0], acc[1] };
+    const int32_t *const p2[2] = { psq[0], psq[1] };
+    oracle_propagate(n, a2, p2, stm, (cnt - 1) / 4, psqt_out, pos_out);
+    return 0;
+}
+
+void oracle_propagate(const onet *n, const int16_t *const acc[2], const int32_t *const psq[2], int stm, int bucket,
+                      int32_t *psqt_out, int32_t *pos_out) {
+    const uint32_t hd = n->hd;
     const int persp[2] = { stm, 1 - stm };
     /* transform(): psqt = (psqtAcc[stm][b] - psqtAcc[~stm][b]) / 2 (C truncation) */
     int32_t psqt = (int32_t)((uint32_t)psq[persp[0]][bucket] - (uint32_t)psq[persp[1]][bucket]) / 2;
@@ -296,7 +317,6 @@ int oracle_eval_board(const onet *n, const uint8_t *board, int stm, int32_t *psq
     int32_t fwd = (int32_t)(((int64_t)y[O_L2 - 1] * (600 * 16)) / (127 * 64));
     *psqt_out = psqt;
     *pos_out = out + fwd;
-    return 0;
 }
 
 /* ---- packed positions (include/fnnue.h fnnue_pos, 36 bytes) ---- */

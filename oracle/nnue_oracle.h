@@ -32,15 +32,30 @@ typedef struct {
 
 typedef struct {
     uint32_t hd;                 /* TransformedFeatureDimensions               */
+    uint32_t nfeat;              /* feature rows: O_FEATURES, or a variant set  */
+    int variant;                 /* 0 chess (HalfKAv2_hm), else OV_* below     */
     uint32_t file_hash;
     char *desc;
     int16_t *ft_bias;            /* [hd]                                       */
-    int16_t *ft_w;               /* [O_FEATURES][hd]                           */
-    int32_t *psqt_w;             /* [O_FEATURES][8]                            */
+    int16_t *ft_w;               /* [nfeat][hd]                                */
+    int32_t *psqt_w;             /* [nfeat][8]                                 */
     ostack st[O_STACKS];
 } onet;
 
 int oracle_make_index(int persp, int s, int pc, int ksq);
 int oracle_eval_board(const onet *n, const uint8_t *board, int stm, int32_t *psqt_out, int32_t *pos_out);
+
+/* Shared by the chess and the variant restatements: FeatureTransformer::
+ * transform + Network[bucket]::propagate from the two perspectives'
+ * accumulators (acc[c] = perspective c's int16[hd], psq[c] its 8 PSQT sums). */
+void oracle_propagate(const onet *n, const int16_t *const acc[2], const int32_t *const psq[2], int stm, int bucket,
+                      int32_t *psqt_out, int32_t *pos_out);
+
+/* ---- Fairy-Stockfish variant nets (variant_oracle.c) ---- */
+#define OV_CRAZYHOUSE 1                /* HalfKAv2 variants, 8x8 + pockets: 64 x 864 */
+#define OV_ATOMIC 2                    /* HalfKAv2 variants, 8x8, no pockets: 64 x 704 */
+#define O_FT_HASH_BASE_VARIANTS 0x5F234CB8u /* HalfKAv2(Variants)::HashValue (recalled) */
+uint32_t oracle_variant_features(int variant);
+int oracle_net_load_variant_mem(const void *buf, size_t len, int variant, onet **out);
 
 #endif

@@ -59,10 +59,25 @@ def _load() -> C.CDLL:
     lib.oracle_board_from_fen.restype = C.c_int
     lib.oracle_apply_uci.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p]
     lib.oracle_apply_uci.restype = C.c_int
+    lib.oracle_net_load_variant_mem.argtypes = [vp, C.c_size_t, C.c_int, C.POINTER(vp)]
+    lib.oracle_net_load_variant_mem.restype = C.c_int
+    lib.voracle_eval_packed.argtypes = [vp, vp, C.c_size_t, vp, vp, C.c_int]
+    lib.voracle_eval_packed.restype = C.c_int
+    lib.voracle_eval_groups.argtypes = [vp, vp, vp, C.c_size_t, C.c_int, vp, vp]
+    lib.voracle_eval_groups.restype = C.c_int
+    lib.voracle_features.argtypes = [C.c_int, vp, C.c_int, vp]
+    lib.voracle_features.restype = C.c_int
+    lib.voracle_board_index.argtypes = [C.c_int] * 5
+    lib.voracle_board_index.restype = C.c_int
+    lib.voracle_hand_index.argtypes = [C.c_int] * 6
+    lib.voracle_hand_index.restype = C.c_int
     return lib
 
 
 lib = _load()
+
+VARIANT_CRAZYHOUSE, VARIANT_ATOMIC = 1, 2
+VPOS_BYTES = 48
 
 
 class OracleNet:
@@ -133,6 +148,49 @@ class OracleNet:
         if getattr(self, "_h", None) and self._h.value and lib is not None:
             lib.oracle_net_free(self._h)
             self._h = C.c_void_p()
+
+
+class VariantOracleNet:
+    """Fairy-Stockfish variant net (variant_oracle.c restatement; parity unpinned)."""
+
+    def __init__(self, data: bytes, variant: int):
+        self._h = C.c_void_p()
+        buf = C.create_string_buffer(data, len(data))
+        rc = lib.oracle_net_load_variant_mem(buf, len(data), variant, C.byref(self._h))
+        if rc != 0:
+            raise ValueError(f"oracle rejected variant net (code {rc})")
+        self.variant = variant
+        self.hd = lib.oracle_net_hd(self._h)
+
+    def eval_packed(self, vpos: np.ndarray, threads: int = 1):
+        vpos = np.ascontiguousarray(vpos, dtype=np.uint8).reshape(-1, VPOS_BYTES)
+        n = vpos.shape[0]
+        ps, po = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        rc = lib.voracle_eval_packed(self._h, vpos.ctypes.data, n, ps.ctypes.data, po.ctypes.data, threads)
+        return ps, po, rc
+
+    def eval_groups(self, vpos: np.ndarray, off: np.ndarray, mode: int):
+        vpos = np.ascontiguousarray(vpos, dtype=np.uint8).reshape(-1, VPOS_BYTES)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = vpos.shape[0]
+        ps, po = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        rc = lib.voracle_eval_groups(self._h, vpos.ctypes.data, off.ctypes.data, len(off) - 1, mode,
+                                     ps.ctypes.data, po.ctypes.data)
+        return ps, po, rc
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value and lib is not None:
+            lib.oracle_net_free(self._h)
+            self._h = C.c_void_p()
+
+
+def variant_features(variant: int, vpos48: np.ndarray, persp: int) -> list[int]:
+    out = np.zeros(64, dtype=np.int32)
+    p = np.ascontiguousarray(vpos48, dtype=np.uint8)
+    k = lib.voracle_features(variant, p.ctypes.data, persp, out.ctypes.data)
+    if k < 0:
+        raise ValueError("invalid variant position")
+    return sorted(out[:k].tolist())
 
 
 def unpack(pos36: np.ndarray) -> tuple[np.ndarray, int]:
