@@ -23,6 +23,10 @@ int cpu_simd_eval_packed(const onet* n, const uint8_t* packed, size_t count, int
 int cpu_simd_eval_groups(const onet* n, const uint8_t* packed, const uint32_t* off, size_t ngroups, int mode,
                          int32_t* psqt, int32_t* positional, int threads);
 int cpu_simd_set_isa(int isa512);
+int voracle_eval_packed(const onet* n, const uint8_t* packed, size_t count, int32_t* psqt, int32_t* positional,
+                        int threads);
+int voracle_eval_groups(const onet* n, const uint8_t* packed, const uint32_t* off, size_t ngroups, int mode,
+                        int32_t* psqt, int32_t* positional);
 }
 
 using namespace fnnue;
@@ -144,6 +148,39 @@ int main() {
       onet* on2 = nullptr;
       CHECK(oracle_net_load_mem(cut.data(), cut.size(), &on2) != 0 && !on2, "oracle rejects a truncated net");
     }
+  }
+  // ---- Fairy-Stockfish variant nets: product parser/writer, variant restatement ----
+  for (int variant : {kVariantCrazyhouse, kVariantAtomic}) {
+    Net vn;
+    synthesize_net(11, 256, 0, vn, variant);
+    std::vector<uint8_t> vbuf;
+    write_net(vn, variant == kVariantCrazyhouse, vbuf);
+    Net back;
+    std::string err;
+    CHECK(parse_net(vbuf.data(), vbuf.size(), back, err, variant) == 0, "variant net round trip");
+    CHECK(parse_net(vbuf.data(), vbuf.size(), back, err, kVariantChess) != 0, "variant net is not a chess net");
+    CHECK(accumulator_bound(back.ft_w.data(), back.ft_bias.data(), back.hd, variant) < 32768, "variant bound");
+    onet* von = nullptr;
+    CHECK(oracle_net_load_variant_mem(vbuf.data(), vbuf.size(), variant, &von) == 0, "variant oracle loads");
+    if (!von) continue;
+    // start position (white / black to move) and kings only with 15 pieces in each hand (48-B records)
+    std::vector<uint8_t> vp(48 * 3, 0);
+    const uint8_t start[32] = {0x24, 0x53, 0x36, 0x42, 0x11, 0x11, 0x11, 0x11, 0, 0, 0, 0, 0, 0, 0, 0,
+                               0,    0,    0,    0,    0,    0,    0,    0,    0x99, 0x99, 0x99, 0x99,
+                               0xAC, 0xDB, 0xBE, 0xCA};
+    std::memcpy(vp.data(), start, 32);
+    std::memcpy(vp.data() + 48, start, 32);
+    vp[48 + 32] = 1;
+    vp[96 + 2] = 0x06;   // white king on e1 (square 4 = low nibble of byte 2)
+    vp[96 + 30] = 0xE0;  // black king on f8 (square 61 = high nibble of byte 30)
+    if (variant == kVariantCrazyhouse)
+      for (int i = 0; i < 10; ++i) vp[96 + 33 + i] = i % 5 == 0 ? 7 : 2;
+    std::vector<int32_t> a(3), b(3), c(3), d(3);
+    (void)voracle_eval_packed(von, vp.data(), 3, a.data(), b.data(), 2);
+    const uint32_t off[2] = {0, 3};
+    (void)voracle_eval_groups(von, vp.data(), off, 1, 0, c.data(), d.data());
+    CHECK(a == c && b == d, "variant incremental == refresh");
+    oracle_net_free(von);
   }
   if (failures) {
     std::fprintf(stderr, "%d check(s) failed\n", failures);

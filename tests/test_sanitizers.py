@@ -19,7 +19,7 @@ SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-f
 def test_host_code_under_asan_ubsan(tmp_path):
     out = tmp_path / "san_main"
     objs = []
-    for src in ("oracle/nnue_oracle.c", "oracle/nnue_cpu_simd.c"):
+    for src in ("oracle/nnue_oracle.c", "oracle/nnue_cpu_simd.c", "oracle/variant_oracle.c"):
         o = tmp_path / (os.path.basename(src) + ".o")
         subprocess.run(["gcc", "-std=c11", *SAN, "-c", os.path.join(ROOT, src), "-o", str(o)], check=True)
         objs.append(str(o))
