@@ -54,7 +54,10 @@ __global__ __launch_bounds__(1024) void plan_count_kernel(const fnnue_pos* __res
     if (h[i]) atomicAdd(&ctr[kCnt + i], h[i]);
 }
 
-// Item record: (n << 24) | (slot << 1) | half, half 0 = side-to-move half of x.
+// Item record: (n << 24) | (bucket << 21) | (slot << 1) | half, half 0 =
+// side-to-move half of x; n = list length + 1 (pieces, + pieces in hand for
+// variants), bucket = the PSQT / layer-stack bucket (pieces on board - 1) / 4
+// (slot < 2^20: chunk_for_hd).
 // One lane per position; the workgroup's 256 positions get local ranks from
 // LDS atomics, then reserve one range per bin with a single global atomic.
 __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
@@ -104,8 +107,8 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
   write_rows(b, 0, b.wk, iw, ctr, flist);
   write_rows(b, 1, b.bk, ib, ctr, flist);
 #endif
-  items[iw] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 0);
-  items[ib] = ((uint32_t)b.cnt << 24) | (slot << 1) | (uint32_t)(b.stm != 1);
+  items[iw] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 0);
+  items[ib] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;
   // the PSQT term is summed from LDS by the slice-0 workgroups of ft_slices
 }
@@ -144,9 +147,9 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     lo = swar_unpack4(lo);
     hi = swar_unpack4(hi);
   }
-  // (rec & 0xFFFFFF) = 2 * slot + half: times HD/2 it is the offset of the
+  // (rec & kItemRowMask) = 2 * slot + half: times HD/2 it is the offset of the
   // item's half of row `slot` of x.
-  const uint32_t xoff = (rec & 0xFFFFFFu) * (HD / 2) + 32 * s + 4 * q;
+  const uint32_t xoff = (rec & kItemRowMask) * (HD / 2) + 32 * s + 4 * q;
 #ifdef FT_EXP_NO_STORE
   if (transform4(lo, hi) == 0x12345678u)
 #endif
@@ -160,7 +163,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32
     // wrap).  The item's 8 lanes take entries q, q+8, q+16, q+24 (padding
     // entries name the zero row) and reduce over lane masks 1, 2, 12.
-    const int bucket = (max((int)(rec >> 24), 1) - 1) >> 2;
+    const int bucket = (int)((rec >> 21) & 7u);
     const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
     acc = q == 0 ? (uint32_t)ptile[krow * kPsqtBuckets + bucket] : 0u;  // own king
 #pragma unroll
@@ -172,7 +175,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
   // Slices != 0 address past the buffer's range: the hardware drops the store
   // (raw buffer bounds check), so every pass issues the same store with no
   // branch and no memory traffic.
-  const uint32_t poff = s == 0 ? (rec & 0xFFFFFFu) * 4u : kDroppedOffset;
+  const uint32_t poff = s == 0 ? (rec & kItemRowMask) * 4u : kDroppedOffset;
   __builtin_amdgcn_raw_buffer_store_b32((int32_t)acc, psqt_rsrc, poff, 0, 0);
 }
 

@@ -38,6 +38,8 @@ constexpr int kBins = kItemBins + kPosBins;
 #endif
 constexpr int kScatterPositions = PLAN_WG;    // positions per plan_scatter workgroup (one per lane)
 
+constexpr uint32_t kItemRowMask = 0x1FFFFF;  // item record bits 0..20: 2 * slot + half (ft_sliced.hip)
+
 // Counter block layout (uint32 words).
 constexpr int kCnt = 0, kOff = kBins, kCur = 2 * kBins, kNUnits = 3 * kBins;
 

@@ -88,7 +88,7 @@ __device__ __forceinline__ void vwrite_rows(const VariantBoard& v, int persp, ui
       }
     }
   }
-  for (; k < 32; ++k) put(R);
+  while (k < 32) put(R);  // put() advances k
   uint4* dst = reinterpret_cast<uint4*>(flist + (size_t)it * 32);
 #pragma unroll
   for (int q = 0; q < 4; ++q) dst[q] = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
@@ -218,9 +218,10 @@ __global__ __launch_bounds__(kScatterPositions) void vplan_scatter_kernel(
   const uint32_t ppb = (ib - ctr[kVOff + vblock(1, v.b.bk) * 33]) & 1u;
   vwrite_rows<R>(v, 0, iw, ppw, flist);
   vwrite_rows<R>(v, 1, ib, ppb, flist);
-  items[iw] = ((uint32_t)v.nfeat << 24) | (slot << 1) | (uint32_t)(v.b.stm != 0);
-  items[ib] = ((uint32_t)v.nfeat << 24) | (slot << 1) | (uint32_t)(v.b.stm != 1);
-  bucket_out[slot] = (uint8_t)((v.b.cnt - 1) >> 2);
+  const uint32_t bucket = (uint32_t)(v.b.cnt - 1) >> 2;  // pieces on board only
+  items[iw] = ((uint32_t)v.nfeat << 24) | (bucket << 21) | (slot << 1) | (uint32_t)(v.b.stm != 0);
+  items[ib] = ((uint32_t)v.nfeat << 24) | (bucket << 21) | (slot << 1) | (uint32_t)(v.b.stm != 1);
+  bucket_out[slot] = (uint8_t)bucket;
 }
 
 }  // namespace
