@@ -24,6 +24,9 @@ Other workloads (the other BASELINE configs, measured for DESIGN.md):
   --workload games     config 3: random-playout games, every ply, incremental (CHAIN)
   --workload children  config 4: every ply of random games plus all legal children (STAR)
   --small-net 128      also evaluate every position with a small net each step (config 3's big + small)
+  --workload crazyhouse / atomic
+                       config 5: Fairy-Stockfish HalfKAv2-variants nets (synthetic), 1M random-walk
+                       variant positions per GPU (pockets / explosions), from scratch
 
 roofline: the binding resource of the dominant kernel (ft_slices for config
 2, ft_segments for configs 3/4) from the committed PMC profile of this tree
@@ -61,8 +64,8 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["positions", "games", "children"], default="positions")
-    ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions workload)")
+    ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic"], default="positions")
+    ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions / variant workloads)")
     ap.add_argument("--games", type=int, default=10_000, help="games per GPU (games / children workloads)")
     ap.add_argument("--hd", type=int, default=1024)
     ap.add_argument("--small-net", type=int, default=0, metavar="HD",
@@ -179,9 +182,16 @@ class Shard:
         self.small = torch.zeros(2, self.n, dtype=torch.int32, device=dev) if small else None
 
 
+def variant_of(F, workload):
+    return {"crazyhouse": F.VARIANT_CRAZYHOUSE, "atomic": F.VARIANT_ATOMIC}.get(workload)
+
+
 def make_inputs(F, args, seed, threads):
     off = None
-    if args.workload == "positions":
+    variant = variant_of(F, args.workload)
+    if variant is not None:
+        pos = F.random_vpositions(seed, variant, args.positions, 160)
+    elif args.workload == "positions":
         pos = F.random_playouts(seed, args.positions, 0, 160, threads=threads)
     else:
         mode = F.PLAYOUT_PLIES if args.workload == "games" else F.PLAYOUT_CHILDREN
@@ -214,7 +224,10 @@ def main():
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    groups = args.workload != "positions"
+    variant = variant_of(F, args.workload)
+    if variant is not None and args.small_net:
+        raise SystemExit("--small-net applies to the chess workloads")
+    groups = args.workload in ("games", "children")
     gmode = None if not groups else (F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR)
 
     # ---- net: rank 0 / device 0 holds it, RCCL broadcasts it over xGMI ----
@@ -223,6 +236,16 @@ def main():
     nets = [(args.seed, args.hd)] + ([(args.seed + 1000, args.small_net)] if args.small_net else [])
     evs = []  # per net: list of per-device contexts
     for seed, hd in nets:
+        if variant is not None:
+            # variant nets: every rank / device builds its context from the net
+            # file (fnnue_multi RCCL-broadcasts the image for the devices launch)
+            vnet = F.Net.from_bytes_variant(F.synthesize_variant_net(seed, hd, variant), variant)
+            if launch == "devices":
+                multi = F.MultiEvaluator(vnet, devices)
+                evs.append([multi.ctx(i) for i in range(len(devices))])
+            else:
+                evs.append([F.Evaluator(vnet, local)])
+            continue
         if launch == "devices":
             m = F.MultiEvaluator(F.Net.from_bytes(F.synthesize_net(seed, hd, 0)), devices)
             if multi is None:
@@ -237,7 +260,7 @@ def main():
             torch.cuda.synchronize()
             evs.append([F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=hd)])
             del img
-    for e in evs[0]:
+    for e in evs[0] if variant is None else []:
         e.set_ft_impl(F._native.FT_GATHER if args.ft_impl == "gather" else F._native.FT_SLICED)
     t_net = time.time() - t0
 
@@ -252,7 +275,14 @@ def main():
         shards.append(Shard(torch, torch.device("cuda", d), pos, off, args.small_net))
     pos, off = host0
     board = boards_of(pos)
-    if not groups:
+    if variant is not None:
+        hand = pos[:, 33:43].astype(np.int64).sum(axis=1)
+        rows = rows_scratch(board) + 2 * hand
+        workload = ("BASELINE config 5: %s random-walk positions (pseudo-legal moves, %s; L~U[0,160]), "
+                    "from-scratch accumulators, synthetic Fairy-Stockfish HalfKAv2-variants net (HD=%d)"
+                    % (args.workload, "drops and captures to hand" if args.workload == "crazyhouse"
+                       else "explosions", args.hd))
+    elif not groups:
         rows = rows_scratch(board)
         workload = ("BASELINE config 2: random-playout positions (splitmix64, L~U[0,160]), from-scratch "
                     "accumulators, synthetic SFNNv5 net (HalfKAv2_hm, HD=%d)" % args.hd)
@@ -277,7 +307,11 @@ def main():
 
     def run_net(k):
         outs = [(s.psqt, s.positional) if k == 0 else (s.small[0], s.small[1]) for s in shards]
-        if launch == "devices":
+        if variant is not None:  # device entry point per GPU (async; ctx streams for fnnue_multi)
+            for s, e, o in zip(shards, evs[k], outs):
+                e.eval_vpositions_device(s.pos.data_ptr(), s.n, o[0].data_ptr(), o[1].data_ptr(),
+                                         None if launch == "devices" else torch.cuda.current_stream().cuda_stream)
+        elif launch == "devices":
             m = multi if k == 0 else multi_small
             if not groups:
                 m.eval_positions_device([s.pos.data_ptr() for s in shards], [s.n for s in shards],
@@ -376,7 +410,27 @@ def main():
                                        if rc2 == 0 else None}}
 
     cpu, parity = None, None
-    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and variant is not None:
+        from oracle.oracle import VariantOracleNet  # cpu_baseline leg: the scalar C restatement is the CPU port
+        on = VariantOracleNet(F.synthesize_variant_net(args.seed, args.hd, variant), variant)
+        done, mism, t0 = 0, 0, time.perf_counter()
+        while True:
+            lo = done % npos
+            hi = min(lo + 20_000, npos)
+            ps, po, rc = on.eval_packed(pos[lo:hi], threads=threads)
+            assert rc == 0
+            mism += int(((ps != psqt[lo:hi]) | (po != positional[lo:hi])).sum())
+            done += hi - lo
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        cpu_el = time.perf_counter() - t0
+        cpu = {"value": done / cpu_el, "unit": "positions/s", "cores": threads, "kind": "port",
+               "cpu": {k: cpus[k] for k in ("model", "os_cpu_count", "affinity", "cgroup_quota", "omp_num_threads")},
+               "sample": f"{done} positions of the same workload (from-scratch refresh per position; {cpu_el:.1f} s "
+                         f"wall on {threads} threads; oracle/variant_oracle.c = scalar C restatement of "
+                         f"Fairy-Stockfish's HalfKAv2-variants NNUE, -O3, no SIMD: Fairy-Stockfish itself is absent)"}
+        parity = {"checked": min(done, npos), "mismatches": mism}
+    elif rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
         from oracle.oracle import OracleNet  # cpu_baseline leg: oracle/nnue_cpu_simd.c is the timed CPU port
         from oracle.oracle import lib as olib
         isa = "AVX-512 VNNI" if olib.cpu_simd_isa512() else "AVX2"
@@ -413,6 +467,12 @@ def main():
                          f"NNUE code paths restated (register-tiled accumulators, maddubs/VPDPBUSD affine), -O3; "
                          f"bit-identical to the scalar oracle)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
+    elif rank == 0 and launch == "devices" and variant is not None:
+        from oracle.oracle import VariantOracleNet
+        on = VariantOracleNet(F.synthesize_variant_net(args.seed, args.hd, variant), variant)
+        k = min(npos, 50_000)
+        ops, opo, rc = on.eval_packed(pos[:k], threads=threads)
+        parity = {"checked": k, "mismatches": int(((ops != psqt[:k]) | (opo != positional[:k])).sum())}
     elif rank == 0 and launch == "devices":
         # spot check of device 0's shard against the oracle (test infrastructure)
         from oracle.oracle import OracleNet
@@ -424,7 +484,7 @@ def main():
     # The host-buffer entry points (host arrays in and out over PCIe, validity
     # checked on the device) — reported beside `value`, never as it.
     host_api = None
-    if not dist_on and not args.no_host_api:
+    if not dist_on and not args.no_host_api and not (variant is not None and launch == "devices"):
         reps = 3
         hpos = pos if launch != "devices" else np.concatenate([pos] * len(devices))
         hoff = off
@@ -433,11 +493,14 @@ def main():
         target = multi if launch == "devices" else evs[0][0]
         t0 = time.perf_counter()
         for _ in range(reps):
-            hp, hq = target.eval_positions(hpos) if not groups else target.eval_groups(hpos, hoff, gmode)
+            if variant is not None:
+                hp, hq = target.eval_vpositions(hpos)
+            else:
+                hp, hq = target.eval_positions(hpos) if not groups else target.eval_groups(hpos, hoff, gmode)
         host_el = time.perf_counter() - t0
         host_api = {"value": len(hpos) * reps / host_el, "unit": "positions/s",
                     "same_results": bool(np.array_equal(hp[:npos], psqt) and np.array_equal(hq[:npos], positional)),
-                    "note": "host (pageable numpy) buffers through the C ABI: H2D 36 B + D2H 8 B per position "
+                    "note": f"host (pageable numpy) buffers through the C ABI: H2D {pos.shape[1]} B + D2H 8 B per position "
                             "over PCIe around the same kernels"
                             + (" (fnnue_multi: one host thread per GPU, results into disjoint slices)"
                                if launch == "devices" else "")}
@@ -503,7 +566,7 @@ def main():
                            "devices": "one process, fnnue_multi over %d GPUs (RCCL broadcast inside the C ABI)"
                                       % n_gpus,
                            "single": "one process, one GPU"}[launch],
-                "ft_impl": args.ft_impl if not groups else "groups",
+                "ft_impl": "groups" if groups else ("sliced (variant tiles)" if variant is not None else args.ft_impl),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
