@@ -3,7 +3,7 @@
 #   usage: tools/exp_run.sh name1 name2 ...   (extra bench args in $BENCH_ARGS)
 mkdir -p gpurun_out/exp
 for v in "$@"; do
-  FNNUE_LIB=$PWD/exp/libfnnue_$v.so timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} \
+  FNNUE_LIB=$PWD/exp/libfnnue_$v.so timeout -k 10 300 python bench.py --cpu-seconds 1 --no-host-api ${BENCH_ARGS:-} \
     > gpurun_out/exp/$v.log 2>&1
   rc=$?
   python3 - "$v" "$rc" <<'PY'
