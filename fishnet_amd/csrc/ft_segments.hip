@@ -433,6 +433,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   __shared__ int32_t ptile[kTileRows * kPsqtBuckets];
   __shared__ uint2 lbuf[16][64];
   __shared__ uint4 dbuf[16][8 * kDbufStride];  // per wave: 8 positions' delta records of its 8 items
+  __shared__ uint32_t claim;  // next pass of the unit to hand out
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;
@@ -465,6 +466,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
     const int s = (int)(j % S);
     if (unit >= nunits) return;
     __syncthreads();  // the previous unit's tile reads are done before the reload
+    if (threadIdx.x == 0) claim = 16;
     const int4 u = units[unit];
     const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
     uint4 t[kTileLoads];
@@ -481,7 +483,13 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
     const int krow = king_row(u.x);
     const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
     const int last = u.z - 1;
-    int base = u.y + wv * 8;
+    // Passes are handed out longest first (items are sorted by length bin, so
+    // from the unit's end backwards), the next one claimed from an LDS counter
+    // when the current one starts: waves finish within one pass of each other.
+    const int npass = (u.z - u.y + 7) / 8;
+    auto pass_base = [&](int k) { return k < npass ? u.y + (npass - 1 - k) * 8 : (int)u.z; };
+    int kp = wv;
+    int base = pass_base(kp);
     SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
 #pragma unroll
     for (int k = 0; k < kTileLoads; ++k)
@@ -503,14 +511,18 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
     }
     while (base < u.z) {
       const SegFetch cur = fa;
-      fa = fetch_seg(items_rsrc, flist_rsrc, base + 128, last, lane, it_in_wave);
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(&claim, 1u);
+      kp = __builtin_amdgcn_readfirstlane((int)c);
+      const int next = pass_base(kp);
+      fa = fetch_seg(items_rsrc, flist_rsrc, next, last, lane, it_in_wave);
       if (s == 0)
         seg_pass<HD, kStar, true>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
                                   x_rsrc, drec_rsrc, dbuf[wv]);
       else
         seg_pass<HD, kStar, false>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
                                    x_rsrc, drec_rsrc, dbuf[wv]);
-      base += 128;
+      base = next;
     }
   }
 }
