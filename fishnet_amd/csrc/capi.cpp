@@ -504,7 +504,7 @@ int fnnue_ctx_set_swar(fnnue_ctx* ctx, int enable) {
 
 int fnnue_net_accumulator_bound(const fnnue_net* net, int32_t* bound) {
   if (!net || !bound) return fail(FNNUE_E_ARG, "null argument");
-  *bound = accumulator_bound(net->net.ft_w.data(), net->net.ft_bias.data(), net->net.hd);
+  *bound = accumulator_bound(net->net.ft_w.data(), net->net.ft_bias.data(), net->net.hd, net->net.variant);
   return FNNUE_OK;
 }
 

@@ -116,3 +116,34 @@ def test_random_vpositions_are_valid():
     assert np.all((b == 6).sum(1) == 1) and np.all((b == 14).sum(1) == 1)
     at = F.random_vpositions(3, ATOMIC, 3000, 160)
     assert at[:, 33:43].sum() == 0
+
+
+def numpy_accumulator_bound(data: bytes, hd: int, rows: int, blocks: int, king_row) -> int:
+    """The SWAR bound restated over the raw file: per king block and even
+    column, |bias + own-king row| + the 31 largest |w| of the other rows."""
+    desc_len = int(np.frombuffer(data, np.uint32, 1, 8)[0])
+    o = 12 + desc_len + 4  # header, then the FT hash
+    bias = np.frombuffer(data, np.int16, hd, o).astype(np.int64)
+    w = np.frombuffer(data, np.int16, blocks * rows * hd, o + 2 * hd).reshape(blocks, rows, hd)[:, :, 0::2]
+    w = np.abs(w.astype(np.int64))
+    worst = 0
+    for kb in range(blocks):
+        kr = king_row(kb)
+        m = w[kb].copy()
+        base = np.abs(bias[0::2] + np.frombuffer(data, np.int16, hd, o + 2 * hd + 2 * (kb * rows + kr) * hd)[0::2])
+        m[kr] = 0
+        top = -np.sort(-m, axis=0)[:31].sum(axis=0)
+        worst = max(worst, int((base + top).max()))
+    return worst
+
+
+@pytest.mark.parametrize("variant,rows", [(CZH, 864), (ATOMIC, 704)])
+def test_variant_accumulator_bound_covers_the_whole_table(variant, rows):
+    """fnnue_net_accumulator_bound of a variant net runs over its 64 king
+    blocks of `rows` rows (own king row 640 + king square)."""
+    data = F.synthesize_variant_net(4, 256, variant)
+    got = F.Net.from_bytes_variant(data, variant).accumulator_bound()
+    assert got == numpy_accumulator_bound(data, 256, rows, 64, lambda kb: 640 + kb)
+    chess = net_bytes(7, 128, 0)
+    assert F.Net.from_bytes(chess).accumulator_bound() == numpy_accumulator_bound(
+        chess, 128, 704, 32, lambda kb: 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3)))
