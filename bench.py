@@ -37,6 +37,7 @@ measured here with HIP events on its launch stream; `frac` = the largest.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import importlib.util
 import json
 import os
@@ -182,6 +183,20 @@ class Shard:
         self.small = torch.zeros(2, self.n, dtype=torch.int32, device=dev) if small else None
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """RCCL prints a version banner on stdout when a communicator is created;
+    the bench's stdout is its one JSON line, so fd 1 points at stderr meanwhile."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def variant_of(F, workload):
     return {"crazyhouse": F.VARIANT_CRAZYHOUSE, "atomic": F.VARIANT_ATOMIC}.get(workload)
 
@@ -223,7 +238,8 @@ def main():
     dist_on = launch == "ranks"
     if dist_on:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     variant = variant_of(F, args.workload)
     if variant is not None and args.small_net:
         raise SystemExit("--small-net applies to the chess workloads")
@@ -241,13 +257,15 @@ def main():
             # file (fnnue_multi RCCL-broadcasts the image for the devices launch)
             vnet = F.Net.from_bytes_variant(F.synthesize_variant_net(seed, hd, variant), variant)
             if launch == "devices":
-                multi = F.MultiEvaluator(vnet, devices)
+                with stdout_to_stderr():
+                    multi = F.MultiEvaluator(vnet, devices)
                 evs.append([multi.ctx(i) for i in range(len(devices))])
             else:
                 evs.append([F.Evaluator(vnet, local)])
             continue
         if launch == "devices":
-            m = F.MultiEvaluator(F.Net.from_bytes(F.synthesize_net(seed, hd, 0)), devices)
+            with stdout_to_stderr():
+                m = F.MultiEvaluator(F.Net.from_bytes(F.synthesize_net(seed, hd, 0)), devices)
             if multi is None:
                 multi = m
             else:
@@ -256,7 +274,8 @@ def main():
         else:
             dev = torch.device("cuda", local)
             image = F.Net.from_bytes(F.synthesize_net(seed, hd, 0)).image() if rank == 0 else None
-            img = D.broadcast_image(image, dev) if dist_on else torch.from_numpy(image).to(dev)
+            with stdout_to_stderr():
+                img = D.broadcast_image(image, dev) if dist_on else torch.from_numpy(image).to(dev)
             torch.cuda.synchronize()
             evs.append([F.Evaluator(None, local, image_ptr=img.data_ptr(), image_bytes=img.numel(), hd=hd)])
             del img
@@ -307,10 +326,13 @@ def main():
 
     def run_net(k):
         outs = [(s.psqt, s.positional) if k == 0 else (s.small[0], s.small[1]) for s in shards]
-        if variant is not None:  # device entry point per GPU (async; ctx streams for fnnue_multi)
-            for s, e, o in zip(shards, evs[k], outs):
-                e.eval_vpositions_device(s.pos.data_ptr(), s.n, o[0].data_ptr(), o[1].data_ptr(),
-                                         None if launch == "devices" else torch.cuda.current_stream().cuda_stream)
+        if variant is not None and launch == "devices":
+            multi.eval_vpositions_device([s.pos.data_ptr() for s in shards], [s.n for s in shards],
+                                         [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs])
+        elif variant is not None:
+            s, e = shards[0], evs[k][0]
+            e.eval_vpositions_device(s.pos.data_ptr(), s.n, outs[0][0].data_ptr(), outs[0][1].data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream)
         elif launch == "devices":
             m = multi if k == 0 else multi_small
             if not groups:
@@ -484,7 +506,7 @@ def main():
     # The host-buffer entry points (host arrays in and out over PCIe, validity
     # checked on the device) — reported beside `value`, never as it.
     host_api = None
-    if not dist_on and not args.no_host_api and not (variant is not None and launch == "devices"):
+    if not dist_on and not args.no_host_api:
         reps = 3
         hpos = pos if launch != "devices" else np.concatenate([pos] * len(devices))
         hoff = off
@@ -494,7 +516,7 @@ def main():
         t0 = time.perf_counter()
         for _ in range(reps):
             if variant is not None:
-                hp, hq = target.eval_vpositions(hpos)
+                hp, hq = target.eval_vpositions(hpos)  # fnnue_multi_eval_vpositions for the devices launch
             else:
                 hp, hq = target.eval_positions(hpos) if not groups else target.eval_groups(hpos, hoff, gmode)
         host_el = time.perf_counter() - t0

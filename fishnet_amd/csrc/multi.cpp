@@ -219,6 +219,26 @@ int fnnue_multi_eval_groups_device(fnnue_multi* m, const fnnue_pos* const* d_pos
   return FNNUE_OK;
 }
 
+int fnnue_multi_eval_vpositions(fnnue_multi* m, const fnnue_vpos* pos, size_t n, int32_t* psqt, int32_t* positional) {
+  if (!m) return fail(FNNUE_E_ARG, "null multi");
+  if (n == 0) return FNNUE_OK;
+  if (!pos || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
+  const size_t nd = m->ctx.size();
+  return per_device(m, [&](size_t i) {
+    const size_t lo = n * i / nd, hi = n * (i + 1) / nd;
+    return fnnue_eval_vpositions(m->ctx[i], pos + lo, hi - lo, psqt + lo, positional + lo);
+  });
+}
+
+int fnnue_multi_eval_vpositions_device(fnnue_multi* m, const fnnue_vpos* const* d_pos, const size_t* n,
+                                       int32_t* const* d_psqt, int32_t* const* d_positional) {
+  if (!m || !d_pos || !n || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null argument");
+  for (size_t i = 0; i < m->ctx.size(); ++i)
+    if (int rc = fnnue_eval_vpositions_device(m->ctx[i], d_pos[i], n[i], d_psqt[i], d_positional[i], nullptr))
+      return fail(rc, "device " + std::to_string(m->devices[i]) + ": " + fnnue_last_error());
+  return FNNUE_OK;
+}
+
 int fnnue_multi_sync(fnnue_multi* m) {
   if (!m) return fail(FNNUE_E_ARG, "null multi");
   int first = FNNUE_OK;

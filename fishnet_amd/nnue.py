@@ -315,6 +315,14 @@ class MultiEvaluator:
         N.check(N.lib.fnnue_multi_eval_positions(self._h, N.ptr(pos), n, N.ptr(psqt), N.ptr(positional)))
         return psqt, positional
 
+    def eval_vpositions(self, vpos: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        vpos = np.ascontiguousarray(vpos, dtype=np.uint8).reshape(-1, N.VPOS_BYTES)
+        n = vpos.shape[0]
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_multi_eval_vpositions(self._h, N.ptr(vpos), n, N.ptr(psqt), N.ptr(positional)))
+        return psqt, positional
+
     def eval_groups(self, pos: np.ndarray, off: np.ndarray, mode: int = N.GROUP_CHAIN):
         pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
         off = np.ascontiguousarray(off, dtype=np.uint32)
@@ -331,6 +339,10 @@ class MultiEvaluator:
     def eval_positions_device(self, d_pos, n, d_psqt, d_positional) -> None:
         N.check(N.lib.fnnue_multi_eval_positions_device(self._h, _ptrs(d_pos), _sizes(n), _ptrs(d_psqt),
                                                         _ptrs(d_positional)))
+
+    def eval_vpositions_device(self, d_pos, n, d_psqt, d_positional) -> None:
+        N.check(N.lib.fnnue_multi_eval_vpositions_device(self._h, _ptrs(d_pos), _sizes(n), _ptrs(d_psqt),
+                                                         _ptrs(d_positional)))
 
     def eval_groups_device(self, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional) -> None:
         N.check(N.lib.fnnue_multi_eval_groups_device(self._h, _ptrs(d_pos), _ptrs(d_off), _sizes(ngroups),

@@ -178,6 +178,12 @@ int fnnue_multi_eval_groups_device(fnnue_multi *m, const fnnue_pos *const *d_pos
                                    const size_t *ngroups, const size_t *npos, int mode, int32_t *const *d_psqt,
                                    int32_t *const *d_positional);
 int fnnue_multi_sync(fnnue_multi *m);
+/* Fairy-Stockfish variant positions over every device of a multi built from a
+ * variant net (BASELINE config 5 on 8 GPUs): contiguous shards, as
+ * fnnue_multi_eval_positions[_device]. */
+int fnnue_multi_eval_vpositions(fnnue_multi *m, const fnnue_vpos *pos, size_t n, int32_t *psqt, int32_t *positional);
+int fnnue_multi_eval_vpositions_device(fnnue_multi *m, const fnnue_vpos *const *d_pos, const size_t *n,
+                                       int32_t *const *d_psqt, int32_t *const *d_positional);
 /* Splits groups off[0..ngroups] into nparts contiguous runs of whole groups
  * with about equal position counts: part k = groups [cut[k], cut[k+1]),
  * cut has nparts + 1 entries.  Host only. */

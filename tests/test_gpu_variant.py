@@ -115,5 +115,15 @@ def test_variant_multi_device(vcache):
         ps, po = m.ctx(0).eval_vpositions(pos)
         ops, opo, rc = VariantOracleNet(data, CZH).eval_packed(pos, threads=8)
         assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+        mps, mpo = m.eval_vpositions(pos)  # fnnue_multi_eval_vpositions (host buffers, sharded)
+        assert np.array_equal(mps, ops) and np.array_equal(mpo, opo)
+        import torch
+        dev = torch.device("cuda", 0)
+        d_pos = torch.from_numpy(pos).to(dev)
+        d_ps = torch.zeros(len(pos), dtype=torch.int32, device=dev)
+        d_po = torch.zeros(len(pos), dtype=torch.int32, device=dev)
+        m.eval_vpositions_device([d_pos.data_ptr()], [len(pos)], [d_ps.data_ptr()], [d_po.data_ptr()])
+        m.sync()
+        assert np.array_equal(d_ps.cpu().numpy(), ops) and np.array_equal(d_po.cpu().numpy(), opo)
     finally:
         m.close()
