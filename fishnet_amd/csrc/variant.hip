@@ -58,37 +58,42 @@ __device__ __forceinline__ int vplane(int persp, int pc) {
 
 // Perspective `persp`'s list: every feature but the own king, as 16 * row
 // (row relative to the king block), padded with the zero row R; rows of parity
-// pp first (the bank pairing of ft_slices, see write_rows).
+// pp first (the bank pairing of ft_slices, see write_rows).  The entries are
+// gathered in the thread's own LDS row (`mine`, 68-B stride: a wave's rows
+// start in 32 different banks) because their count per source is data
+// dependent — a register array indexed by a divergent k costs a waterfall loop
+// per entry — then read back as 16 words with static indices.
+constexpr int kVListStrideWords = 17;
+
 template <int R>
 __device__ __forceinline__ void vwrite_rows(const VariantBoard& v, int persp, uint32_t it, uint32_t pp,
-                                            uint16_t* __restrict__ flist) {
+                                            uint32_t* __restrict__ mine, uint16_t* __restrict__ flist) {
   const int ksq = persp ? v.b.bk : v.b.wk;
   const uint64_t occ = v.b.occ & ~(1ull << ksq);
   constexpr uint64_t kEvenFiles = 0x5555555555555555ull;
-  uint32_t E[16];
+  uint16_t* L = reinterpret_cast<uint16_t*>(mine);
   int k = 0;
-  auto put = [&](uint32_t row) {
-    const uint32_t a = 16u * row;
-    if (k & 1) E[k >> 1] |= a << 16;
-    else E[k >> 1] = a;
-    ++k;
-  };
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     const uint32_t want = pass == 0 ? pp : pp ^ 1u;  // row parity = file parity (rank flip keeps files)
     for (uint64_t m = occ & (want ? ~kEvenFiles : kEvenFiles); m; m &= m - 1) {
       const int s = __builtin_ctzll(m);
-      put((uint32_t)(vblock(persp, s) + 64 * vplane(persp, nibble_at(v.b.w, s))));
+      L[k++] = (uint16_t)(16u * (uint32_t)(vblock(persp, s) + 64 * vplane(persp, nibble_at(v.b.w, s))));
     }
     if (R > kVBoardRows) {
+#pragma unroll
       for (int i = 0; i < 10; ++i) {
         const int owner = i >= 5, pt = i % 5;
         const uint32_t base = kVBoardRows + kVHandSlots * (2 * pt + (owner != persp));
-        for (uint32_t c = want; c < v.hand[i]; c += 2) put(base + c);  // row parity = c & 1
+        for (uint32_t c = want; c < v.hand[i]; c += 2) L[k++] = (uint16_t)(16u * (base + c));  // row parity = c & 1
       }
     }
   }
-  while (k < 32) put(R);  // put() advances k
+  for (; k < 32; ++k) L[k] = (uint16_t)(16u * R);
+  uint32_t E[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j)  // this thread's own LDS writes (same type: no aliasing reorder), in order
+    E[j] = (uint32_t)L[2 * j] | (uint32_t)L[2 * j + 1] << 16;
   uint4* dst = reinterpret_cast<uint4*>(flist + (size_t)it * 32);
 #pragma unroll
   for (int q = 0; q < 4; ++q) dst[q] = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
@@ -182,6 +187,7 @@ __global__ __launch_bounds__(kScatterPositions) void vplan_scatter_kernel(
     int32_t* __restrict__ psqt_out) {
   __shared__ uint32_t lcnt[kVBins];
   __shared__ uint32_t lbase[kVBins];
+  __shared__ uint32_t lists[kScatterPositions * kVListStrideWords];
   for (int i = threadIdx.x; i < kVBins; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
   const uint32_t p = blockIdx.x * kScatterPositions + threadIdx.x;
@@ -216,8 +222,9 @@ __global__ __launch_bounds__(kScatterPositions) void vplan_scatter_kernel(
   // starts are multiples of kUnitItems from there, so pass items 2k / 2k + 1)
   const uint32_t ppw = (iw - ctr[kVOff + vblock(0, v.b.wk) * 33]) & 1u;
   const uint32_t ppb = (ib - ctr[kVOff + vblock(1, v.b.bk) * 33]) & 1u;
-  vwrite_rows<R>(v, 0, iw, ppw, flist);
-  vwrite_rows<R>(v, 1, ib, ppb, flist);
+  uint32_t* mine = lists + threadIdx.x * kVListStrideWords;
+  vwrite_rows<R>(v, 0, iw, ppw, mine, flist);
+  vwrite_rows<R>(v, 1, ib, ppb, mine, flist);
   const uint32_t bucket = (uint32_t)(v.b.cnt - 1) >> 2;  // pieces on board only
   items[iw] = ((uint32_t)v.nfeat << 24) | (bucket << 21) | (slot << 1) | (uint32_t)(v.b.stm != 0);
   items[ib] = ((uint32_t)v.nfeat << 24) | (bucket << 21) | (slot << 1) | (uint32_t)(v.b.stm != 1);

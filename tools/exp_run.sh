@@ -12,7 +12,7 @@ v, rc = sys.argv[1], sys.argv[2]
 try:
     line = [l for l in open(f"gpurun_out/exp/{v}.log") if l.startswith("{")][-1]
     d = json.loads(line)
-    print(f"{v:12s} rc={rc} {d['value']/1e6:8.1f}M/s ft={d['roofline']['kernel_avg_ms']:.4f} ms stack={d['roofline']['stack_kernel_avg_ms']:.4f} mism={(d.get('parity_spot_check') or {}).get('mismatches')}")
+    print(f"{v:12s} rc={rc} {d['value']/1e6:8.1f}M/s plan={d['roofline']['plan_avg_ms']:.4f} ft={d['roofline']['kernel_avg_ms']:.4f} ms stack={d['roofline']['stack_kernel_avg_ms']:.4f} mism={(d.get('parity_spot_check') or {}).get('mismatches')}")
 except Exception as e:
     print(v, "rc", rc, "no result", e)
 PY
