@@ -234,6 +234,7 @@ __global__ __launch_bounds__(1024) void seg_scatter_kernel(const fnnue_pos* __re
                                                            uint16_t* __restrict__ flist) {
   __shared__ uint32_t lcnt[kItemBins];
   __shared__ uint32_t lbase[kItemBins];
+  __shared__ uint32_t lists[1024 * kListStrideWords];  // write_rows staging, one row per lane
   const uint32_t K = cref[2 * n], K0 = cref[n];
   if (blockIdx.x * blockDim.x >= K) return;  // workgroup-uniform
   for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) lcnt[i] = 0;
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(1024) void seg_scatter_kernel(const fnnue_pos* __re
   const uint32_t slot = lbase[key] + rk;
   const uint32_t half = b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(b.cnt - 1) >> 2;
   items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)b.cnt);
-  write_rows(b, (int)c, c ? b.bk : b.wk, slot, ctr, flist);
+  write_rows(b, (int)c, c ? b.bk : b.wk, slot, ctr, lists + threadIdx.x * kListStrideWords, flist);
 }
 
 struct SegFetch {

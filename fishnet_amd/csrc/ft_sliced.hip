@@ -67,6 +67,7 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
                                                            int32_t* __restrict__ psqt_out) {
   __shared__ uint32_t lcnt[kBins];
   __shared__ uint32_t lbase[kBins];
+  __shared__ uint32_t lists[kScatterPositions * kListStrideWords];  // write_rows staging, one row per lane
   for (int i = threadIdx.x; i < kBins; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
   const uint32_t p = blockIdx.x * kScatterPositions + threadIdx.x;
@@ -103,10 +104,9 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
   }
   const int bucket = (b.cnt - 1) >> 2;
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
-#ifndef FT_EXP_NO_ROWS_WRITE
-  write_rows(b, 0, b.wk, iw, ctr, flist);
-  write_rows(b, 1, b.bk, ib, ctr, flist);
-#endif
+  uint32_t* mine = lists + threadIdx.x * kListStrideWords;
+  write_rows(b, 0, b.wk, iw, ctr, mine, flist);
+  write_rows(b, 1, b.bk, ib, ctr, mine, flist);
   items[iw] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;

@@ -267,6 +267,8 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
   }
 }
 
+constexpr int kListStrideWords = 17;  // words per lane of the list staging rows (68 B)
+
 // Writes item `it`'s 32 feature-list entries (rows relative to its king block,
 // padded with the zero row): every piece except the perspective's own king,
 // whose row is the same for the whole king block (king_row) and is added to
@@ -276,31 +278,38 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
 // odd rows first: the pair then mostly reads opposite bank halves.  A row's
 // parity is (square ^ mirror) & 1 (orient() flips files when the king is on
 // files a-d), and the sum is order-independent.
+// The entries are gathered in the thread's own LDS row (`mine`,
+// kListStrideWords words: the rows of a wave start in 32 different banks), one
+// step per piece, then the padding, and read back with static indices (a
+// register array indexed by the divergent entry count would cost selects or
+// waterfall loops per entry): plan_scatter 8 us faster than 32 select steps.
 __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ksq, uint32_t it,
-                                           const uint32_t* __restrict__ ctr, uint16_t* __restrict__ flist) {
+                                               const uint32_t* __restrict__ ctr, uint32_t* __restrict__ mine,
+                                               uint16_t* __restrict__ flist) {
   const int kbc = king_block(persp, ksq);
   const uint32_t pp = (it - ctr[kOff + kbc * 33]) & 1;
   const uint32_t mirror = (ksq & 7) < 4 ? 1u : 0u;
+  const int flip = (persp ? 56 : 0) ^ (mirror ? 7 : 0);
   constexpr uint64_t kEvenFiles = 0x5555555555555555ull;
-  const uint64_t occ = b.occ & ~(1ull << ksq);  // own king: folded into the bias (king_row)
-  uint64_t first = occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
-  uint64_t second = occ & ~first;
+  const uint64_t occ = b.occ & ~(1ull << ksq);
+  const uint64_t first = occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
+  uint16_t* L = reinterpret_cast<uint16_t*>(mine);
+  int k = 0;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass)
+    for (uint64_t m = pass == 0 ? first : occ & ~first; m; m &= m - 1) {
+      const int sq = __builtin_ctzll(m);
+      const int pc = nibble_at(b.w, sq), type = pc & 7;
+      const int plane = type == 6 ? 10 : 2 * (type - 1) + ((pc >> 3) != persp);
+      L[k++] = (uint16_t)(16u * (uint32_t)((sq ^ flip) + 64 * plane));
+    }
+  for (; k < 32; ++k) L[k] = (uint16_t)kNoEntry;
   uint32_t E[16];
 #pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    uint32_t a = kNoEntry;
-    if (first | second) {
-      uint64_t& m = first ? first : second;
-      const int sq = __builtin_ctzll(m);
-      m &= m - 1;
-      a = 16u * (uint32_t)(make_index(persp, sq, nibble_at(b.w, sq), ksq) - kRowsPerBlock * kbc);
-    }
-    if (k & 1) E[k >> 1] |= a << 16;
-    else E[k >> 1] = a;
-  }
+  for (int j = 0; j < 16; ++j) E[j] = (uint32_t)L[2 * j] | (uint32_t)L[2 * j + 1] << 16;
   uint4* dst = reinterpret_cast<uint4*>(flist + (size_t)it * 32);
 #pragma unroll
-  for (int k = 0; k < 4; ++k) dst[k] = make_uint4(E[4 * k], E[4 * k + 1], E[4 * k + 2], E[4 * k + 3]);
+  for (int q = 0; q < 4; ++q) dst[q] = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
 }
 
 // Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
