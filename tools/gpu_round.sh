@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r02f; mkdir -p $O
+O=gpurun_out/${ROUND_TAG:-r02x}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread > $O/gputest.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/gputest.log; exit 1; }
 tail -3 $O/gputest.log
 for wl in positions games children crazyhouse atomic; do
