@@ -49,20 +49,47 @@ __global__ __launch_bounds__(64 * kWaves) void xread(const uint8_t* __restrict__
   if (v == 0x7F3A5C11) atomicAdd(out, 1);
 }
 
+// Fills x the way ft_slices does (every byte written once, 4 B per lane) so
+// the read that follows starts with dirty lines in L2 / the Infinity Cache.
+__global__ __launch_bounds__(256) void xwrite(uint8_t* __restrict__ x, size_t words, uint32_t v) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(x);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < words; i += (size_t)gridDim.x * blockDim.x)
+    w[i] = v ^ (uint32_t)i;
+}
+
+template <int kShape, int kWaves>
+float run_dirty(uint8_t* x, uint32_t n, int* out, int reps) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  float tot = 0;
+  for (int r = 0; r < reps; ++r) {
+    hipLaunchKernelGGL(xwrite, dim3(4096), dim3(256), 0, 0, x, (size_t)n * HD / 4, (uint32_t)r);
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL((xread<kShape, kWaves>), dim3(256), dim3(64 * kWaves), 0, 0, x, n, out);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    tot += ms;
+  }
+  return tot / reps;
+}
+
 template <int kShape, int kWaves>
 float run(const uint8_t* x, uint32_t n, int* out, int reps) {
   hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
   const int blocks = 256;
   hipLaunchKernelGGL((xread<kShape, kWaves>), dim3(blocks), dim3(64 * kWaves), 0, 0, x, n, out);
-  hipEventRecord(a, 0);
+  (void)hipEventRecord(a, 0);
   for (int r = 0; r < reps; ++r)
     hipLaunchKernelGGL((xread<kShape, kWaves>), dim3(blocks), dim3(64 * kWaves), 0, 0, x, n, out);
-  hipEventRecord(b, 0);
-  hipEventSynchronize(b);
+  (void)hipEventRecord(b, 0);
+  (void)hipEventSynchronize(b);
   float ms = 0;
-  hipEventElapsedTime(&ms, a, b);
+  (void)hipEventElapsedTime(&ms, a, b);
   return ms / reps;
 }
 
@@ -71,8 +98,8 @@ int main() {
   uint8_t* x = nullptr;
   int* out = nullptr;
   if (hipMalloc(&x, (size_t)n * HD) != hipSuccess || hipMalloc(&out, 4) != hipSuccess) return 1;
-  hipMemset(x, 3, (size_t)n * HD);
-  hipMemset(out, 0, 4);
+  (void)hipMemset(x, 3, (size_t)n * HD);
+  (void)hipMemset(out, 0, 4);
   const double gb = (double)n * HD / 1e9;
   const char* names[3] = {"mfma 16x64B", "row128 8x128B", "flat 1x1KiB"};
   for (int rep = 0; rep < 2; ++rep) {
@@ -90,9 +117,15 @@ int main() {
       printf("%-14s waves 8: %.1f us %.2f TB/s | 12: %.1f us %.2f TB/s | 16: %.1f us %.2f TB/s\n", names[s],
              t[s][0] * 1e3, gb / t[s][0], t[s][1] * 1e3, gb / t[s][1], t[s][2] * 1e3, gb / t[s][2]);
   }
+  {
+    const float d0 = run_dirty<0, 12>(x, n, out, 10), d1 = run_dirty<1, 12>(x, n, out, 10),
+                d2 = run_dirty<2, 12>(x, n, out, 10);
+    printf("after a 1 GiB write, 12 waves: mfma %.1f us %.2f TB/s | row128 %.1f us %.2f TB/s | flat %.1f us %.2f TB/s\n",
+           d0 * 1e3, gb / d0, d1 * 1e3, gb / d1, d2 * 1e3, gb / d2);
+  }
   hipError_t e = hipDeviceSynchronize();
   printf("status %s\n", hipGetErrorString(e));
-  hipFree(x);
-  hipFree(out);
+  (void)hipFree(x);
+  (void)hipFree(out);
   return e == hipSuccess ? 0 : 1;
 }
