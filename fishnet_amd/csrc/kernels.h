@@ -39,10 +39,16 @@ hipError_t launch_stack(uint32_t hd, const uint8_t* x, const uint8_t* bucket, ui
                         hipStream_t stream);
 
 // LDS-stationary feature transformer (ft_sliced.hip).
+// Perspective-items per (king block) work unit: 48 passes of 128 items.
+// Measured on config 2 (1M positions): 4096 595-600M, 5120 586-592M, 6144
+// 603-613M, 7168 594-599M, 8192 592-597M positions/s (crazyhouse: neutral).
+// Must stay a multiple of 128 (a pass step) so pass items 2k / 2k + 1 keep
+// their parity roles (write_rows).
 #ifndef FT_UNIT_ITEMS
-#define FT_UNIT_ITEMS 4096
+#define FT_UNIT_ITEMS 6144
 #endif
-constexpr uint32_t kUnitItems = FT_UNIT_ITEMS;  // perspective-items per (king block) work unit
+constexpr uint32_t kUnitItems = FT_UNIT_ITEMS;
+static_assert(kUnitItems % 128 == 0, "units are whole pass steps");
 struct SlicedPlan {
   void* tiles;       // [32 king blocks][hd/64 slices][705 rows][8] x 16 B (relayout of ft_w)
   uint32_t* ctr;     // sliced_ctr_words() counters / offsets
