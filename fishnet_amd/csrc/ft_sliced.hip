@@ -143,17 +143,14 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
   }
   u16x4 lo = b_lo, hi = b_hi;
   rows_sum<kSwar>(maxn - 1, e, base, lo, hi);  // maxn - 1 rows (own king in the bias); wave-uniform, straight-line
-  if constexpr (kSwar) {
-    lo = swar_unpack4(lo);
-    hi = swar_unpack4(hi);
-  }
   // (rec & kItemRowMask) = 2 * slot + half: times HD/2 it is the offset of the
   // item's half of row `slot` of x.
   const uint32_t xoff = (rec & kItemRowMask) * (HD / 2) + 32 * s + 4 * q;
+  const uint32_t xv = kSwar ? transform4_swar(lo, hi) : transform4(lo, hi);
 #ifdef FT_EXP_NO_STORE
-  if (transform4(lo, hi) == 0x12345678u)
+  if (xv == 0x12345678u)
 #endif
-  __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xoff, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(xv, x_rsrc, xoff, 0, 0);
   uint32_t acc = 0;
 #ifdef FT_EXP_NO_PSQT
   if (false) {
@@ -268,6 +265,10 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
       b_hi = swar_words(b_hi);
     }
     accum_row<kSwar>(kv, b_lo, b_hi);
+    if constexpr (kSwar) {  // both halves of every word offset by 0x8000 (transform4_swar)
+      b_lo = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_lo) + kSwarOffset);
+      b_hi = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_hi) + kSwarOffset);
+    }
   }
   while (base < u.z) {
     const PassFetch cur = fa;

@@ -410,20 +410,29 @@ constexpr int kRowDepth = 4 * FT_DEPTH;
 // v_add_u32 per word instead of a VOP3P v_pk_add_u16, which issues at ~1.75x
 // its cost).  The sum is exact mod 2^32; while the true sum of column c stays
 // within int16 range its low half is that sum and the high half, after the
-// low half's sign is taken back out (swar_unpack), is column c+1's sum mod
-// 2^16 — the int16 wraparound of upstream's accumulator.
+// low half's sign is taken back out (transform4_swar), is column c+1's sum
+// mod 2^16 — the int16 wraparound of upstream's accumulator.
 __device__ __forceinline__ uint32_t swar_word(uint32_t packed) { return packed - ((packed & 0x8000u) << 1); }
-__device__ __forceinline__ uint32_t swar_unpack(uint32_t w) {
-  const uint32_t h = w - (uint32_t)(int32_t)(int16_t)(uint16_t)w;  // low 16 bits zero
-  return h | (w & 0xFFFFu);
-}
 __device__ __forceinline__ u16x4 swar_words(u16x4 v) {
   const u32x2 w = __builtin_bit_cast(u32x2, v);
   return __builtin_bit_cast(u16x4, u32x2{swar_word(w.x), swar_word(w.y)});
 }
-__device__ __forceinline__ u16x4 swar_unpack4(u16x4 v) {
-  const u32x2 w = __builtin_bit_cast(u32x2, v);
-  return __builtin_bit_cast(u16x4, u32x2{swar_unpack(w.x), swar_unpack(w.y)});
+
+// Transform straight from SWAR words.  The accumulator starts at the bias plus
+// kSwarOffset (0x80008000 per word): a word w = l + 65536 h (l signed, the
+// exact low column; h the high column mod 2^16) then holds l + 0x8000 in its
+// low half (the 0x8000 carries out of the low half exactly when l < 0,
+// restoring the borrow a negative l took from the high half) and h + 0x8000
+// in its high half, both mod 2^16.  A saturating u16 subtract of 0x8000 is
+// max(column, 0) on both halves at once, so no unpacking is needed.
+constexpr uint32_t kSwarOffset = 0x80008000u;
+__device__ __forceinline__ uint32_t transform4_swar(u16x4 lo, u16x4 hi) {
+  const u16x4 off = (u16x4)0x8000, top = (u16x4)127;
+  const u16x4 a = __builtin_elementwise_min(__builtin_elementwise_sub_sat(lo, off), top);
+  const u16x4 b = __builtin_elementwise_min(__builtin_elementwise_sub_sat(hi, off), top);
+  const u16x4 pr = (a * b) << (u16x4)1;
+  const u32x2 w = __builtin_bit_cast(u32x2, pr);
+  return __builtin_amdgcn_perm(w.y, w.x, 0x07050301u);
 }
 
 template <bool kSwar = false>
