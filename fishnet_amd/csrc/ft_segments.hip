@@ -285,20 +285,37 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 // One delta position: cur = base -/+ the removed / added rows of record d.
 // kAdd2 = false when no record of the batch has a second added piece (only
-// the other side's castling has one), which skips that row.
-template <bool kAdd2>
+// the other side's castling has one), which skips that row.  kSwar: rows and
+// accumulators are SWAR words (sliced_common.h), so each column pair costs
+// 32-bit VOP2 adds / subtracts instead of VOP3P packed ones; every
+// intermediate is a subset sum of one position's features, inside the bound
+// that enabled SWAR.
+template <bool kAdd2, bool kSwar>
 __device__ __forceinline__ void apply_delta(const char* lbase, const uint4& d, u16x4 b_lo, u16x4 b_hi, u16x4& lo,
                                             u16x4& hi) {
   const u32x4 r0 = *row_addr(lbase, d.y, 0), r1 = *row_addr(lbase, d.y, 1);
   const u32x4 a0 = *row_addr(lbase, d.z, 0);
-  auto lo2 = [](const u32x4& v) { return __builtin_bit_cast(u16x4, __builtin_shufflevector(v, v, 0, 1)); };
-  auto hi2 = [](const u32x4& v) { return __builtin_bit_cast(u16x4, __builtin_shufflevector(v, v, 2, 3)); };
-  lo = b_lo - lo2(r0) - lo2(r1) + lo2(a0);
-  hi = b_hi - hi2(r0) - hi2(r1) + hi2(a0);
-  if constexpr (kAdd2) {
-    const u32x4 a1 = *row_addr(lbase, d.z, 1);
-    lo += lo2(a1);
-    hi += hi2(a1);
+  auto lo2 = [](const u32x4& v) { return __builtin_shufflevector(v, v, 0, 1); };
+  auto hi2 = [](const u32x4& v) { return __builtin_shufflevector(v, v, 2, 3); };
+  if constexpr (kSwar) {
+    u32x2 l = __builtin_bit_cast(u32x2, b_lo) - (lo2(r0) + lo2(r1)) + lo2(a0);
+    u32x2 h = __builtin_bit_cast(u32x2, b_hi) - (hi2(r0) + hi2(r1)) + hi2(a0);
+    if constexpr (kAdd2) {
+      const u32x4 a1 = *row_addr(lbase, d.z, 1);
+      l += lo2(a1);
+      h += hi2(a1);
+    }
+    lo = __builtin_bit_cast(u16x4, l);
+    hi = __builtin_bit_cast(u16x4, h);
+  } else {
+    auto c = [](u32x2 v) { return __builtin_bit_cast(u16x4, v); };
+    lo = b_lo - c(lo2(r0)) - c(lo2(r1)) + c(lo2(a0));
+    hi = b_hi - c(hi2(r0)) - c(hi2(r1)) + c(hi2(a0));
+    if constexpr (kAdd2) {
+      const u32x4 a1 = *row_addr(lbase, d.z, 1);
+      lo += c(lo2(a1));
+      hi += c(hi2(a1));
+    }
   }
 }
 
@@ -316,7 +333,7 @@ __device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4&
 // their rows into the zero row and their stores out of range (dropped).
 constexpr int kDbufStride = 9;  // records per item in the per-wave LDS buffer (8 + 1 padding)
 
-template <int HD, bool kStar, bool kPsqt>
+template <int HD, bool kStar, bool kPsqt, bool kSwar>
 __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
                                          int q, uint32_t n, const char* lbase, u16x4 b_lo, u16x4 b_hi, int krow,
                                          const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
@@ -337,9 +354,9 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     e[4 * m + 3] = v.w;
   }
   u16x4 lo = b_lo, hi = b_hi;
-  rows_sum((int)maxn - 1, e, lbase, lo, hi);
+  rows_sum<kSwar>((int)maxn - 1, e, lbase, lo, hi);
   const uint32_t col = 32 * s + 4 * q;
-  __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc,
+  __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc,
                                         ((rec.x & kSlotMask) * 2 + ((rec.x >> 24) & 1)) * (HD / 2) + col, 0, 0);
   int32_t p = 0;
   auto psqt_off = [&](uint32_t x, bool live) {
@@ -388,9 +405,9 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
       const uint4 d = db[jj];  // past the segment's end: the sentinel record (seg_members_kernel)
-      apply_delta<kAdd2>(lbase, d, blo, bhi, lo, hi);
+      apply_delta<kAdd2, kSwar>(lbase, d, blo, bhi, lo, hi);
       const uint32_t xo = (d.x & kRowMask) * (HD / 2) + col;
-      __builtin_amdgcn_raw_buffer_store_b32(transform4(lo, hi), x_rsrc, xo, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc, xo, 0, 0);
       int32_t pc = 0;
       if constexpr (kPsqt) {
         pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta<kAdd2>(ptile, d, q));
@@ -418,7 +435,7 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   }
 }
 
-template <int HD, bool kStar>
+template <int HD, bool kStar, bool kSwar>
 __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restrict__ tiles,
                                                            const int16_t* __restrict__ ftb,
                                                            const uint32_t* __restrict__ ctr,
@@ -494,7 +511,11 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
     SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
 #pragma unroll
     for (int k = 0; k < kTileLoads; ++k)
-      if ((int)threadIdx.x + 1024 * k < kTileU4) img[threadIdx.x + 1024 * k] = t[k];
+      if ((int)threadIdx.x + 1024 * k < kTileU4) {
+        uint4 v = t[k];
+        if constexpr (kSwar) v = make_uint4(swar_word(v.x), swar_word(v.y), swar_word(v.z), swar_word(v.w));
+        img[threadIdx.x + 1024 * k] = v;
+      }
     if (s == 0) {
       uint4* pdst = reinterpret_cast<uint4*>(ptile);
 #pragma unroll
@@ -504,11 +525,17 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       }
     }
     __syncthreads();
-    {
+    {  // the own-king row (every item of the unit has it) joins the bias
       const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
-      const u32x2 klo = __builtin_shufflevector(kv, kv, 0, 1), khi = __builtin_shufflevector(kv, kv, 2, 3);
-      b_lo += __builtin_bit_cast(u16x4, klo);
-      b_hi += __builtin_bit_cast(u16x4, khi);
+      if constexpr (kSwar) {
+        b_lo = swar_words(b_lo);
+        b_hi = swar_words(b_hi);
+      }
+      accum_row<kSwar>(kv, b_lo, b_hi);
+      if constexpr (kSwar) {  // both halves of every word offset by 0x8000 (transform4_swar)
+        b_lo = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_lo) + kSwarOffset);
+        b_hi = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_hi) + kSwarOffset);
+      }
     }
     while (base < u.z) {
       const SegFetch cur = fa;
@@ -518,11 +545,11 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       const int next = pass_base(kp);
       fa = fetch_seg(items_rsrc, flist_rsrc, next, last, lane, it_in_wave);
       if (s == 0)
-        seg_pass<HD, kStar, true>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
-                                  x_rsrc, drec_rsrc, dbuf[wv]);
+        seg_pass<HD, kStar, true, kSwar>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile,
+                                         psqt_rsrc, x_rsrc, drec_rsrc, dbuf[wv]);
       else
-        seg_pass<HD, kStar, false>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
-                                   x_rsrc, drec_rsrc, dbuf[wv]);
+        seg_pass<HD, kStar, false, kSwar>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile,
+                                          psqt_rsrc, x_rsrc, drec_rsrc, dbuf[wv]);
       base = next;
     }
   }
@@ -534,14 +561,15 @@ hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& n
   constexpr int S = HD / 64;
   // grid = 8 * S * G (see the kernel's grid stride); up to 8 * 64 units per sweep
   const uint32_t groups = min((max_units + 7) / 8, 64u);
+  auto launch = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(groups * 8 * S), dim3(1024), 0, stream, (const uint4*)P.tiles, net.ft_bias, P.ctr,
+                       (const int4*)P.units, (const uint4*)G.items, P.flist, (const uint4*)G.drec, n, net.psqt_w,
+                       P.psqt_part, x);
+  };
   if (star)
-    hipLaunchKernelGGL((ft_segments_kernel<HD, true>), dim3(groups * 8 * S), dim3(1024), 0, stream,
-                       (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, (const uint4*)G.items, P.flist,
-                       (const uint4*)G.drec, n, net.psqt_w, P.psqt_part, x);
+    P.swar ? launch(ft_segments_kernel<HD, true, true>) : launch(ft_segments_kernel<HD, true, false>);
   else
-    hipLaunchKernelGGL((ft_segments_kernel<HD, false>), dim3(groups * 8 * S), dim3(1024), 0, stream,
-                       (const uint4*)P.tiles, net.ft_bias, P.ctr, (const int4*)P.units, (const uint4*)G.items, P.flist,
-                       (const uint4*)G.drec, n, net.psqt_w, P.psqt_part, x);
+    P.swar ? launch(ft_segments_kernel<HD, false, true>) : launch(ft_segments_kernel<HD, false, false>);
   return hipGetLastError();
 }
 
