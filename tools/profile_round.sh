@@ -8,7 +8,7 @@
 #   usage: tools/profile_round.sh <tag> [workload ...]   (default: all three)
 set -uo pipefail
 TAG=${1:-rXX}; shift || true
-WLS=${*:-positions games children crazyhouse}
+WLS=${*:-positions games children crazyhouse atomic}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
