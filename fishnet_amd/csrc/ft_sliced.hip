@@ -25,6 +25,8 @@
 // then stack_kernel (kernels.hip) over the bucket-sorted slots.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "sliced_common.h"
 
 namespace fnnue {
@@ -115,12 +117,11 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
 
 // One pass (8 items per wave) over the LDS tile: the lists go to the wave's
 // LDS buffer, bias + rows, transform, store; in slice 0 also the PSQT part.
-// maxn = the pass's longest list.  Both stores are unconditional: a lane past
+// maxn = the pass's longest list.  The stores are unconditional: a lane past
 // the end of the unit holds the clamped last item and rewrites its identical
-// values, and slices != 0 issue their PSQT store out of the buffer's bounds
-// (dropped by the hardware).  A store skipped on some path would make hipcc's
-// vmcnt bookkeeping wait for every store before the next pass's rows.
-template <int HD, bool kSwar>
+// values (a store skipped on some path would make hipcc's vmcnt bookkeeping
+// wait for every store before the next pass's rows).
+template <int HD, bool kSwar, bool kPsqt>
 __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
                                            int q, const char* base, u16x4 b_lo, u16x4 b_hi, int krow,
                                            const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
@@ -151,29 +152,28 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
   if (xv == 0x12345678u)
 #endif
   __builtin_amdgcn_raw_buffer_store_b32(xv, x_rsrc, xoff, 0, 0);
-  uint32_t acc = 0;
-#ifdef FT_EXP_NO_PSQT
-  if (false) {
-#else
-  if (s == 0) {
-#endif
+#ifndef FT_EXP_NO_PSQT
+  if constexpr (kPsqt) {
     // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32
-    // wrap).  The item's 8 lanes take entries q, q+8, q+16, q+24 (padding
-    // entries name the zero row) and reduce over lane masks 1, 2, 12.
-    const int bucket = (int)((rec >> 21) & 7u);
-    const uint16_t* ent = reinterpret_cast<const uint16_t*>(my);
-    acc = q == 0 ? (uint32_t)ptile[krow * kPsqtBuckets + bucket] : 0u;  // own king
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc += (uint32_t)ptile[(ent[q + 8 * j] >> 4) * kPsqtBuckets + bucket];
-    acc += (uint32_t)__shfl_xor((int)acc, 1);
-    acc += (uint32_t)__shfl_xor((int)acc, 2);
-    acc += (uint32_t)__shfl_xor((int)acc, 12);
+    // wrap), own king included, in the fetch layout: lane l holds entries
+    // 4(l&7) .. +3 of pass item l>>3 (f.lst, padding entries name the zero
+    // row), the 8 lanes of an item are consecutive (DPP reductions), and the
+    // item's record comes from its q = 0 lane in the lane_item layout (items
+    // 0..7 -> lanes 0, 20, 4, 16, 32, 52, 36, 48) by one ds_bpermute.
+    const uint32_t li = (uint32_t)lane >> 3;
+    const int src = (int)(((li & 4u) << 3) + ((0x10041400u >> (8u * (li & 3u))) & 0xFFu));
+    const uint32_t reci = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)rec);
+    const int bk = (int)((reci >> 21) & 7u);
+    auto pw = [&](uint32_t en) { return (uint32_t)ptile[(en >> 4) * kPsqtBuckets + bk]; };
+    uint32_t a2 = (lane & 7) == 0 ? (uint32_t)ptile[krow * kPsqtBuckets + bk] : 0u;  // own king
+    a2 += pw(f.lst.x & 0xFFFFu) + pw(f.lst.x >> 16) + pw(f.lst.y & 0xFFFFu) + pw(f.lst.y >> 16);
+    a2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)a2, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    a2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)a2, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    a2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)a2, 0x141, 0xF, 0xF, false);  // row_half_mirror: quads 0 <-> 1
+    __builtin_amdgcn_raw_buffer_store_b32((int32_t)a2, psqt_rsrc,
+                                          (lane & 7) == 0 ? (reci & kItemRowMask) * 4u : kDroppedOffset, 0, 0);
   }
-  // Slices != 0 address past the buffer's range: the hardware drops the store
-  // (raw buffer bounds check), so every pass issues the same store with no
-  // branch and no memory traffic.
-  const uint32_t poff = s == 0 ? (rec & kItemRowMask) * 4u : kDroppedOffset;
-  __builtin_amdgcn_raw_buffer_store_b32((int32_t)acc, psqt_rsrc, poff, 0, 0);
+#endif
 }
 
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; records and
@@ -270,21 +270,31 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
       b_hi = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_hi) + kSwarOffset);
     }
   }
-  while (base < u.z) {
-    const PassFetch cur = fa;
+  // Slice 0 also sums the PSQT part; the other slices run a copy of the loop
+  // without that code (a runtime branch in the shared loop cost them 8 %).
+  auto run = [&](auto psqt) {
+    constexpr bool kPsqt = decltype(psqt)::value;
+    while (base < u.z) {
+      const PassFetch cur = fa;
 #ifndef FT_EXP_REUSE_LIST
-    fa = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
+      fa = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
 #endif
-    slice_pass<HD, kSwar>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
-    base += 128;
-    if (base >= u.z) break;
-    const PassFetch cur2 = fb;
+      slice_pass<HD, kSwar, kPsqt>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
+      base += 128;
+      if (base >= u.z) break;
+      const PassFetch cur2 = fb;
 #ifndef FT_EXP_REUSE_LIST
-    fb = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
+      fb = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
 #endif
-    slice_pass<HD, kSwar>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
-    base += 128;
-  }
+      slice_pass<HD, kSwar, kPsqt>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
+                                   x_rsrc);
+      base += 128;
+    }
+  };
+  if (s == 0)
+    run(std::true_type{});
+  else
+    run(std::false_type{});
 }
 
 template <int HD>
