@@ -127,3 +127,25 @@ def test_variant_multi_device(vcache):
         assert np.array_equal(d_ps.cpu().numpy(), ops) and np.array_equal(d_po.cpu().numpy(), opo)
     finally:
         m.close()
+
+
+def test_variant_golden_vectors_on_device():
+    """The device path against the committed variant fixture (the same
+    vectors tests/test_variant.py checks the restatement against)."""
+    import hashlib
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_variant_evals.json")))
+    for e in g["nets"]:
+        v = e["variant"]
+        ev = F.Evaluator(F.Net.from_bytes_variant(F.synthesize_variant_net(e["seed"], e["hd"], v), v), 0)
+        try:
+            pos = np.stack([F.vpos_from_fen(v, f) for f in e["fens"]])
+            ps, po = ev.eval_vpositions(pos)
+            assert ps.tolist() == e["psqt"] and po.tolist() == e["positional"]
+            walks = F.random_vpositions(e["walks_seed"], v, e["walks_count"], e["walks_max_plies"])
+            wps, wpo = ev.eval_vpositions(walks)
+            digest = hashlib.sha256(wps.astype("<i4").tobytes() + wpo.astype("<i4").tobytes()).hexdigest()
+            assert digest == e["walks_sha256"]
+        finally:
+            ev.close()

@@ -5,6 +5,10 @@ PARITY UNPINNED: the reference runs variants with Fairy-Stockfish's classical
 eval (src/assets.rs:384-391, src/stockfish.rs:248-260), the Fairy-Stockfish
 submodule is empty and no variant net is pinned; the feature set is recalled
 from Fairy-Stockfish's half_ka_v2_variants (oracle/variant_oracle.c header)."""
+import hashlib
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -147,3 +151,25 @@ def test_variant_accumulator_bound_covers_the_whole_table(variant, rows):
     chess = net_bytes(7, 128, 0)
     assert F.Net.from_bytes(chess).accumulator_bound() == numpy_accumulator_bound(
         chess, 128, 704, 32, lambda kb: 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3)))
+
+
+GOLDEN_V = os.path.join(os.path.dirname(__file__), "golden", "golden_variant_evals.json")
+
+
+def test_variant_golden_vectors():
+    """The restatement against its committed fixture (tests/golden/
+    make_variant_fixtures.py): FENs with holdings, atomic positions and a
+    digest over 4000 random walks per net."""
+    g = json.load(open(GOLDEN_V))
+    assert len(g["nets"]) == 4
+    for e in g["nets"]:
+        v = e["variant"]
+        on = VariantOracleNet(F.synthesize_variant_net(e["seed"], e["hd"], v), v)
+        pos = np.stack([F.vpos_from_fen(v, f) for f in e["fens"]])
+        ps, po, rc = on.eval_packed(pos, threads=4)
+        assert rc == 0 and ps.tolist() == e["psqt"] and po.tolist() == e["positional"]
+        walks = F.random_vpositions(e["walks_seed"], v, e["walks_count"], e["walks_max_plies"])
+        wps, wpo, rc = on.eval_packed(walks, threads=8)
+        assert rc == 0
+        digest = hashlib.sha256(wps.astype("<i4").tobytes() + wpo.astype("<i4").tobytes()).hexdigest()
+        assert digest == e["walks_sha256"]
