@@ -114,6 +114,12 @@ SIGNATURES = {
     "fnnue_random_vpositions": ([_u64, _i32, _sz, _u32, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_eval_vpositions": ([_vp, _vp, _sz, _vp, _vp], _i32),
     "fnnue_eval_vpositions_device": ([_vp, _vp, _sz, _vp, _vp, _vp], _i32),
+    # include/fnnue_backend.h
+    "fnnue_backend_channel": ([_vp, _i32, _vp, _P(_vp)], _i32),
+    "fnnue_backend_free": ([_vp], None),
+    "fnnue_backend_batch_size": ([_vp, _P(_sz)], _i32),
+    "fnnue_backend_go": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp], _i32),
+    "fnnue_backend_analysis_json": ([_vp, _sz, C.c_char_p, _sz, _P(_sz)], _i32),
 }
 
 for _name, (_args, _res) in SIGNATURES.items():

@@ -82,6 +82,8 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant);
 int finish_upload(fnnue_ctx* c);
 // Reads and clears the latched device error word.
 int latched(fnnue_ctx* c);
+// The device's position rule on the host (one king per side, <= 32 pieces, valid codes, stm 0/1).
+bool valid_host_pos(const fnnue_pos& p);
 // After FNNUE_E_POSITION latched: names the first invalid position.
 int name_invalid(int rc, const fnnue_pos* pos, size_t n);
 

@@ -1,0 +1,121 @@
+/* fnnue_backend.h — a batched static-evaluation backend with the shape of
+ * fishnet's engine actor, above the evaluator ABI (fnnue.h).
+ *
+ * The reference sends every position of an acquired batch to a Stockfish
+ * child over UCI, one position per round trip:
+ *   stockfish::channel(exe, StockfishInit{nnue}, logger)
+ *       -> (StockfishStub, StockfishActor)          [ref] src/stockfish.rs:23-38
+ *   StockfishStub::go(Position)
+ *       -> Result<PositionResponse, PositionFailed> [ref] src/stockfish.rs:44-54
+ * with Position / PositionResponse / PositionFailed from src/ipc.rs:16-41,
+ * 100-103, and the batch expanded by IncomingBatch::from_acquired
+ * (src/queue.rs:518-627) from an AcquireResponseBody (src/api.rs:293-309).
+ *
+ * Here the same pair is a channel to one evaluator on one GPU: the actor is a
+ * worker thread owning an fnnue_ctx; a go() sends it whole acquired batches
+ * (capacity-1 channel: a second caller waits, as on the reference's
+ * mpsc::channel(1)) and returns one response per position.  The expansion
+ * (FEN parse, UCI replay, every ply) runs on the device (fnnue_build_batch_
+ * device), the plies are evaluated incrementally along each game (CHAIN
+ * groups), and the two raw NNUE terms become a Score::Cp.  A batch that fails
+ * (unparsable FEN, illegal move, a variant this backend does not evaluate)
+ * gets its own nonzero code in batch_rc — PositionFailed{batch_id}
+ * (queue.rs:207-213 drops that batch) — while the other batches of the call
+ * complete.  A nonzero return of go() itself (device failure) fails them all.
+ *
+ * Score (static evaluation; search is outside this path):
+ *   v  = (psqt + positional) / 16            Stockfish's NNUE value (internal
+ *                                             units, side to move, C division;
+ *                                             upstream evaluate_nnue.cpp with
+ *                                             adjusted = false — the "NNUE
+ *                                             evaluation" the `eval` command
+ *                                             prints)
+ *   cp = v * 100 / normalize_to_pawn         UCI::value's normalisation (upstream
+ *                                             uci.cpp; 361 in SF 15.1 as recalled,
+ *                                             a parameter because it is unpinned)
+ * Analysis work: one response per ply, depth 0, nodes 1, no pv / best move.
+ * Move work: the root after all moves; its legal children are evaluated and
+ * the move maximising -v(child) is the best move (depth 1, nodes = children,
+ * score = that maximum).
+ */
+#ifndef FNNUE_BACKEND_H
+#define FNNUE_BACKEND_H
+
+#include "fnnue.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FNNUE_WORK_ANALYSIS 0 /* Work::Analysis (api.rs:130-143) */
+#define FNNUE_WORK_MOVE 1     /* Work::Move (api.rs:144-151) */
+
+#define FNNUE_SCORE_CP 0      /* Score::Cp (api.rs:383-388) */
+#define FNNUE_SCORE_MATE 1    /* Score::Mate */
+
+typedef struct fnnue_backend fnnue_backend;
+
+/* StockfishInit (stockfish.rs): what the engine is configured with. */
+typedef struct {
+  int32_t normalize_to_pawn; /* cp = v * 100 / normalize_to_pawn; 0 -> 361 */
+  uint32_t reserved;
+} fnnue_backend_init;
+
+/* AcquireResponseBody (api.rs:293-309) of one batch. */
+typedef struct {
+  const char *batch_id;            /* Work::id (BatchId), copied into logs / errors */
+  int work;                        /* FNNUE_WORK_* */
+  int multipv;                     /* Work::Analysis multipv; 0 or 1 (static eval has one line) */
+  const char *position;            /* root FEN (X-FEN / Shredder castling accepted) */
+  const char *variant;             /* "standard", "chess960", "fromPosition", NULL / "" = standard */
+  const char *moves;               /* space-separated UCI (Chess960 king-takes-rook accepted) */
+  const uint32_t *skip_positions;  /* skipPositions: position ids answered as Skipped */
+  size_t nskip;
+} fnnue_acquired;
+
+/* PositionResponse (ipc.rs:28-39) of one position (Skip::Skip when skipped). */
+typedef struct {
+  uint32_t position_id;  /* PositionId: 0 = root, k = after k moves */
+  uint8_t skipped;       /* 1: Skip::Skip (AnalysisPart::Skipped) */
+  uint8_t score_kind;    /* FNNUE_SCORE_* */
+  uint8_t depth;
+  uint8_t pad;
+  int64_t score;         /* centipawns (side to move) */
+  int32_t psqt;          /* the raw NNUE terms the score came from */
+  int32_t positional;
+  uint64_t nodes;
+  uint64_t time_ms;      /* wall time of the go() call */
+  uint32_t nps;          /* positions evaluated per second over the go() call */
+  char best_move[8];     /* UCI, NUL-terminated; "" for analysis */
+} fnnue_position_response;
+
+/* stockfish::channel: starts the actor (worker thread + evaluator on
+ * `device`).  init may be NULL (defaults). */
+int fnnue_backend_channel(const fnnue_net *net, int device, const fnnue_backend_init *init, fnnue_backend **out);
+/* Stops the actor (after the call in flight) and frees it. */
+void fnnue_backend_free(fnnue_backend *b);
+
+/* Number of responses batch `a` expands to (IncomingBatch::from_acquired):
+ * analysis = moves + 1, move = 1.  Host only; FNNUE_E_ARG on a bad work type. */
+int fnnue_backend_batch_size(const fnnue_acquired *a, size_t *n);
+
+/* StockfishStub::go for whole batches.  Batch i's responses land in
+ * out[off[i] .. off[i + 1]) (off: nbatches + 1 entries, filled here; cap =
+ * capacity of out, FNNUE_E_CAPACITY when too small); batch_rc[i] = 0 or the
+ * FNNUE_E_* code of its PositionFailed (its responses then are unspecified).
+ * Thread-safe: concurrent callers queue on the capacity-1 channel. */
+int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nbatches, fnnue_position_response *out,
+                     size_t cap, uint32_t *off, int32_t *batch_rc);
+
+/* The `analysis` array fishnet submits for one analysis batch
+ * (CompletedBatch::into_analysis, queue.rs:715-727; AnalysisPart / Score
+ * serialisation, api.rs:355-388): {"skipped":true} or {"score":{"cp":..},
+ * "depth":..,"nodes":..,"time":..,"nps":..} per position, as JSON.  Writes
+ * at most cap bytes including the NUL; *len = the full length (without NUL);
+ * FNNUE_E_CAPACITY when it did not fit. */
+int fnnue_backend_analysis_json(const fnnue_position_response *r, size_t n, char *buf, size_t cap, size_t *len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

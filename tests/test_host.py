@@ -16,7 +16,8 @@ from tests.positions import CHESS960, FENS, PERFT, START
 
 
 def header_symbols():
-    text = open(os.path.join(ROOT, "include", "fnnue.h")).read()
+    inc = os.path.join(ROOT, "include")
+    text = "".join(open(os.path.join(inc, h)).read() for h in sorted(os.listdir(inc)) if h.endswith(".h"))
     return sorted(set(re.findall(r"\b(fnnue_[a-z0-9_]+)\s*\(", text)))
 
 
