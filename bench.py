@@ -79,8 +79,9 @@ def parse_args():
     ap.add_argument("--threads", type=int, default=0, help="host threads (0 = every core this process may use)")
     ap.add_argument("--ft-impl", choices=["sliced", "gather"], default="sliced",
                     help="feature-transformer kernel for independent positions")
-    ap.add_argument("--launch", choices=["auto", "devices"], default="auto",
-                    help="devices: drive the GPUs through fnnue_multi from this process even at --gpus 1 "
+    ap.add_argument("--launch", choices=["auto", "devices", "ranks"], default="auto",
+                    help="devices: drive the GPUs through fnnue_multi from this process even at --gpus 1; "
+                         "ranks: the torchrun path (RCCL broadcast, max over ranks, gather) even at WORLD_SIZE 1 "
                          "(auto: torchrun ranks if WORLD_SIZE > 1, else fnnue_multi for --gpus > 1)")
     return ap.parse_args()
 
@@ -225,7 +226,10 @@ def main():
     rank, world, local = D.env_rank()
     if world > 1 and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: launch N ranks for N GPUs")
-    launch = "ranks" if world > 1 else ("devices" if args.gpus > 1 or args.launch == "devices" else "single")
+    if args.launch == "ranks" and "MASTER_PORT" not in os.environ:
+        raise SystemExit("--launch ranks needs a torchrun environment (MASTER_ADDR / MASTER_PORT)")
+    launch = "ranks" if world > 1 or args.launch == "ranks" else (
+        "devices" if args.gpus > 1 or args.launch == "devices" else "single")
     ndev_here = args.gpus if launch == "devices" else 1
     have = F.device_count()
     need = (local + 1) if launch != "devices" else args.gpus

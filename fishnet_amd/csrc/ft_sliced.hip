@@ -107,8 +107,10 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
   const int bucket = (b.cnt - 1) >> 2;
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
   uint32_t* mine = lists + threadIdx.x * kListStrideWords;
+#ifndef PLAN_EXP_NO_ROWS
   write_rows(b, 0, b.wk, iw, ctr, mine, flist);
   write_rows(b, 1, b.bk, ib, ctr, mine, flist);
+#endif
   items[iw] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;

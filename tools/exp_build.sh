@@ -15,5 +15,5 @@ for src in *.hip; do
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../exp/libfnnue_$name.so \
-  build/board.o build/net.o build/capi.o build/multi.o build/variant_host.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -lpthread
+  build/board.o build/net.o build/capi.o build/multi.o build/variant_host.o build/backend.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -lpthread
 echo "exp/libfnnue_$name.so"
