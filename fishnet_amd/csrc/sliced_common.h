@@ -269,6 +269,20 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
 
 constexpr int kListStrideWords = 17;  // words per lane of the list staging rows (68 B)
 
+// Plane of piece code pc (0..15) seen from perspective p, one nibble per pc:
+// 2 * (type - 1) + (colour != p), both kings plane 10 (upstream
+// half_ka_v2_hm.h PieceSquareIndex / 64).
+__host__ __device__ constexpr uint64_t plane_table(int persp) {
+  uint64_t t = 0;
+  for (int pc = 1; pc < 16; ++pc) {
+    const int type = pc & 7;
+    if (type < 1 || type > 6) continue;
+    const int plane = type == 6 ? 10 : 2 * (type - 1) + ((pc >> 3) != persp);
+    t |= (uint64_t)plane << (4 * pc);
+  }
+  return t;
+}
+
 // Writes item `it`'s 32 feature-list entries (rows relative to its king block,
 // padded with the zero row): every piece except the perspective's own king,
 // whose row is the same for the whole king block (king_row) and is added to
@@ -279,37 +293,55 @@ constexpr int kListStrideWords = 17;  // words per lane of the list staging rows
 // parity is (square ^ mirror) & 1 (orient() flips files when the king is on
 // files a-d), and the sum is order-independent.
 // The entries are gathered in the thread's own LDS row (`mine`,
-// kListStrideWords words: the rows of a wave start in 32 different banks), one
-// step per piece, then the padding, and read back with static indices (a
-// register array indexed by the divergent entry count would cost selects or
-// waterfall loops per entry): plan_scatter 8 us faster than 32 select steps.
+// kListStrideWords words: the rows of a wave start in 32 different banks),
+// pre-filled with the zero row, then one u16 store per piece at its slot
+// (first-parity pieces from 0, the others from the count of the first), and
+// read back as words.  The pieces are walked rank by rank straight from the
+// packed nibbles (word i = squares 8i..8i+7, nibble j = square 8i+j): the
+// square, piece code and plane come from the bit position and a 64-bit plane
+// table instead of a 64-bit scan plus an 8-way word select per piece
+// (38 -> 18 VALU per piece).
 __device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ksq, uint32_t it,
                                                const uint32_t* __restrict__ ctr, uint32_t* __restrict__ mine,
                                                uint16_t* __restrict__ flist) {
   const int kbc = king_block(persp, ksq);
   const uint32_t pp = (it - ctr[kOff + kbc * 33]) & 1;
   const uint32_t mirror = (ksq & 7) < 4 ? 1u : 0u;
-  const int flip = (persp ? 56 : 0) ^ (mirror ? 7 : 0);
+  const uint32_t flip = (persp ? 56u : 0u) ^ (mirror ? 7u : 0u);
+  const uint64_t ptab = persp ? plane_table(1) : plane_table(0);
   constexpr uint64_t kEvenFiles = 0x5555555555555555ull;
+  const uint32_t fpar = pp ^ mirror;  // square parity listed first
   const uint64_t occ = b.occ & ~(1ull << ksq);
-  const uint64_t first = occ & ((pp ^ mirror) ? ~kEvenFiles : kEvenFiles);
-  uint16_t* L = reinterpret_cast<uint16_t*>(mine);
-  int k = 0;
+  uint32_t kf = 0, ks = (uint32_t)__popcll(occ & (fpar ? ~kEvenFiles : kEvenFiles));
+  // the row is written as u16 and as words: may_alias types keep the
+  // compiler from reordering (or dropping) one kind against the other
+  typedef uint16_t u16_alias __attribute__((__may_alias__));
+  typedef uint32_t u32_alias __attribute__((__may_alias__));
+  u32_alias* M = reinterpret_cast<u32_alias*>(mine);
+  u16_alias* L = reinterpret_cast<u16_alias*>(mine);
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass)
-    for (uint64_t m = pass == 0 ? first : occ & ~first; m; m &= m - 1) {
-      const int sq = __builtin_ctzll(m);
-      const int pc = nibble_at(b.w, sq), type = pc & 7;
-      const int plane = type == 6 ? 10 : 2 * (type - 1) + ((pc >> 3) != persp);
-      L[k++] = (uint16_t)(16u * (uint32_t)((sq ^ flip) + 64 * plane));
+  for (int j = 0; j < 16; ++j) M[j] = kNoEntry | kNoEntry << 16;
+  const uint32_t kw = (uint32_t)ksq >> 3, kbit = 1u << (4 * (ksq & 7));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = b.w[i];
+    uint32_t nz = ((((w & 0x77777777u) + 0x77777777u) | w) >> 3) & 0x11111111u;  // bit 4j: square 8i+j occupied
+    nz &= kw == (uint32_t)i ? ~kbit : ~0u;
+    const uint32_t c16 = ((8u * (uint32_t)i) ^ flip) << 4;
+    while (nz) {
+      const uint32_t bit = (uint32_t)__builtin_ctz(nz);  // 4j
+      nz &= nz - 1;
+      const uint32_t plane = (uint32_t)(ptab >> (((w >> bit) & 15u) << 2)) & 15u;
+      const uint32_t e = ((bit << 2) ^ c16) + (plane << 10);  // 16 * ((8i + j) ^ flip) + 1024 * plane
+      const bool f = ((bit >> 2) & 1u) == fpar;
+      L[f ? kf : ks] = (uint16_t)e;
+      kf += f ? 1u : 0u;
+      ks += f ? 0u : 1u;
     }
-  for (; k < 32; ++k) L[k] = (uint16_t)kNoEntry;
-  uint32_t E[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) E[j] = (uint32_t)L[2 * j] | (uint32_t)L[2 * j + 1] << 16;
+  }
   uint4* dst = reinterpret_cast<uint4*>(flist + (size_t)it * 32);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) dst[q] = make_uint4(E[4 * q], E[4 * q + 1], E[4 * q + 2], E[4 * q + 3]);
+  for (int q = 0; q < 4; ++q) dst[q] = make_uint4(M[4 * q], M[4 * q + 1], M[4 * q + 2], M[4 * q + 3]);
 }
 
 // Number of 16-byte entries of the tile image: 32 king blocks x hd/64 slices
