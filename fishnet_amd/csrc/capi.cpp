@@ -63,7 +63,7 @@ void ctx_destroy(fnnue_ctx* c) {
       if (e) (void)hipEventDestroy(e);
   if (c->ws_event) (void)hipEventDestroy(c->ws_event);
   if (c->stream) (void)hipStreamDestroy(c->stream);
-  for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off,
+  for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off, (void*)c->d_btext,
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
                   (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm,
                   (void*)c->plan.psqt_part, (void*)c->seg.ref, (void*)c->seg.cref, c->seg.dtmp, c->seg.drec,
@@ -158,6 +158,17 @@ int ensure_stage(fnnue_ctx* c, size_t npos, size_t noff) {
       return fail(FNNUE_E_OOM, "device allocation (offsets)");
     c->off_cap = noff;
   }
+  return FNNUE_OK;
+}
+
+// Grow-only staging of fnnue_build_batch's input (text + two offset arrays).
+int ensure_builder_input(fnnue_ctx* c, size_t bytes) {
+  if (bytes <= c->btext_cap) return FNNUE_OK;
+  if (c->d_btext) (void)hipFree(c->d_btext);
+  c->d_btext = nullptr;
+  c->btext_cap = 0;
+  if (hipMalloc(&c->d_btext, bytes) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (builder input)");
+  c->btext_cap = bytes;
   return FNNUE_OK;
 }
 
@@ -992,32 +1003,25 @@ int fnnue_build_batch(fnnue_ctx* ctx, const char* text, size_t text_len, const u
   for (size_t i = 0; i < ngames; ++i)
     if (fen_off[i] > moves_off[i] || moves_off[i] > fen_off[i + 1]) return fail(FNNUE_E_ARG, "offsets out of order");
   DeviceGuard g(ctx->device);
-  struct Bufs {
-    std::vector<void*> p;
-    ~Bufs() {
-      for (void* x : p) (void)hipFree(x);
-    }
-  } B;
-  auto dalloc = [&](size_t bytes) -> void* {
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes ? bytes : 4) != hipSuccess) return nullptr;
-    B.p.push_back(p);
-    return p;
-  };
-  char* d_text = (char*)dalloc(text_len);
-  uint32_t* d_fo = (uint32_t*)dalloc((ngames + 1) * 4);
-  uint32_t* d_mo = (uint32_t*)dalloc(ngames * 4);
-  if (!d_text || !d_fo || !d_mo) return fail(FNNUE_E_OOM, "device allocation (builder input)");
+  // Input and output staging are per-context and grow-only (host-API calls are
+  // synchronous), so a steady stream of batches allocates nothing.
+  const size_t text_bytes = (text_len + 255) / 256 * 256;
+  const size_t fo_bytes = (ngames + 1) * 4, mo_bytes = ngames * 4;
+  int rc = ensure_builder_input(ctx, text_bytes + fo_bytes + mo_bytes);
+  if (rc) return rc;
+  char* d_text = ctx->d_btext;
+  uint32_t* d_fo = reinterpret_cast<uint32_t*>(d_text + text_bytes);
+  uint32_t* d_mo = d_fo + (ngames + 1);
   hipStream_t s = ctx->stream;
   HIP_TRY(hipMemcpyAsync(d_text, text, text_len, hipMemcpyHostToDevice, s), "H2D");
-  HIP_TRY(hipMemcpyAsync(d_fo, fen_off, (ngames + 1) * 4, hipMemcpyHostToDevice, s), "H2D");
-  HIP_TRY(hipMemcpyAsync(d_mo, moves_off, ngames * 4, hipMemcpyHostToDevice, s), "H2D");
-  int rc = fnnue_build_batch_device(ctx, d_text, d_fo, d_mo, ngames, mode, nullptr, 0, nullptr, 0, n_out, n_groups, s);
+  HIP_TRY(hipMemcpyAsync(d_fo, fen_off, fo_bytes, hipMemcpyHostToDevice, s), "H2D");
+  HIP_TRY(hipMemcpyAsync(d_mo, moves_off, mo_bytes, hipMemcpyHostToDevice, s), "H2D");
+  rc = fnnue_build_batch_device(ctx, d_text, d_fo, d_mo, ngames, mode, nullptr, 0, nullptr, 0, n_out, n_groups, s);
   if (rc != FNNUE_E_CAPACITY) return rc;  // sizing pass: always "too small" with no outputs
   if (!out || !off || cap < *n_out || off_cap < *n_groups + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
-  fnnue_pos* d_out = (fnnue_pos*)dalloc(*n_out * sizeof(fnnue_pos));
-  uint32_t* d_off = (uint32_t*)dalloc((*n_groups + 1) * 4);
-  if (!d_out || !d_off) return fail(FNNUE_E_OOM, "device allocation (builder output)");
+  if ((rc = ensure_stage(ctx, *n_out, *n_groups + 1))) return rc;
+  fnnue_pos* d_out = ctx->d_pos;
+  uint32_t* d_off = ctx->d_off;
   rc = fnnue_build_batch_device(ctx, d_text, d_fo, d_mo, ngames, mode, d_out, *n_out, d_off, *n_groups + 1, n_out,
                                 n_groups, s);
   if (rc) return rc;

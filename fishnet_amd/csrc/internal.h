@@ -35,6 +35,8 @@ struct fnnue_ctx {
   int32_t* d_psqt = nullptr;
   int32_t* d_positional = nullptr;
   size_t stage_cap = 0, off_cap = 0;
+  char* d_btext = nullptr;     // fnnue_build_batch input staging (text, then FEN / move offsets), grow-only
+  size_t btext_cap = 0;
   int ft_impl = FNNUE_FT_SLICED;
   int32_t acc_bound = 0;       // accumulator_bound of the net (SWAR rows allowed below 2^15)
   fnnue::SlicedPlan plan{};
