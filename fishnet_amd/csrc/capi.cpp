@@ -611,9 +611,9 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
       std::array<hipEvent_t, 4>* ev = nullptr;
       if ((rc = next_events(ctx, &ev))) return rc;
       if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
-      HIP_TRY(launch_groups_check(d_off, (uint32_t)ngroups, (uint32_t)npos, ctx->err, s), "offset check launch");
       HIP_TRY(launch_ft_segments(ctx->hd, d_pos, (uint32_t)npos, d_off, (uint32_t)ngroups, 0, mode, ctx->ptrs,
-                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
+                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev),
+                                 /*check_offsets=*/true),
               "ft_segments launch");
       return run_chunk_tail(ctx, (uint32_t)npos, d_positional, s, ev, nullptr, ctx->plan.psqt_part, d_psqt);
     }

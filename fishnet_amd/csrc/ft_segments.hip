@@ -17,13 +17,16 @@
 // wrap is a group, so results equal a refresh bit for bit.
 //
 // Plan (all on the device, per chunk of positions):
-//   group_span    per position its group's {first, end} (thread per group)
+//   group_span    per position its group's {first, end} (wave per group);
+//                 zeroes the counters; checks device-only offsets
 //   seg_delta     per (position, perspective): refresh flag or the delta
 //                 record {slot, half, bucket, 2 removed, 2 added rows}
-//   scan          exclusive scan of refresh flags -> item index per refresh
-//   seg_items     item k -> its root position
-//   seg_len       segment length per refresh (next refresh / group parent)
-//   seg_members   delta records placed at root + rank (a segment's plies
+//   scan          exclusive scan of refresh flags -> item index per refresh:
+//                 block counts in seg_delta, seg_scan_blocks, then local
+//                 scans in seg_items_scan, which also maps item k -> its
+//                 root position
+//   seg_place     segment length per refresh (next refresh / group parent);
+//                 delta records placed at root + rank (a segment's plies
 //                 contiguous)
 //   seg_count / plan_scan / seg_scatter   counting sort of items by
 //                 (king block, length bin), unit table cut every
@@ -50,10 +53,27 @@ constexpr uint32_t kRowMask = 0x1FFFFFF;  // delta record x: (2 * slot + half) |
 // Each position's group span {first, end} (chunk-relative), written by
 // group_span_kernel: one wave per group fills its members (coalesced), so the
 // plan kernels read one word pair instead of binary-searching the offsets.
+// The first kernel of the plan, it also zeroes the counter block and the word
+// after ref[2n] (instead of two memset launches) and, with check set (offsets
+// the host never read: fnnue_eval_groups_device with npos <= the workspace),
+// checks them: non-decreasing, off[0] = 0, off[ngroups] = npos, else error
+// bit 2 (FNNUE_E_ARG).
 __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                         uint32_t base, uint32_t n, uint2* __restrict__ span) {
+                                                         uint32_t base, uint32_t n, uint2* __restrict__ span,
+                                                         uint32_t* __restrict__ ctr, uint32_t ctr_words,
+                                                         uint32_t* __restrict__ ref, int check,
+                                                         uint32_t* __restrict__ err) {
+  if (blockIdx.x == 0) {
+    for (uint32_t i = threadIdx.x; i < ctr_words; i += blockDim.x) ctr[i] = 0;
+    if (threadIdx.x == 0) ref[2 * n] = 0;  // the scan then yields cref[2n] = item count
+  }
   const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= ngroups) return;
+  if (check && (threadIdx.x & 63) == 0) {
+    bool bad = off[g + 1] < off[g];
+    if (g == 0) bad |= off[0] != 0 || off[ngroups] != n;
+    if (bad) atomicOr(err, 2u);
+  }
   const uint32_t a = min(off[g] - base, n), b = min(max(off[g + 1] - base, a), n);
   for (uint32_t i = a + (threadIdx.x & 63); i < b; i += 64) span[i] = make_uint2(a, b);
 }
@@ -61,41 +81,28 @@ __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restr
 // The group of position i, clamped to first <= i < end <= n.  With valid
 // offsets the clamp is a no-op; with malformed ones (gaps leave span entries
 // unwritten; the device entry point checks offsets on the device,
-// groups_check_kernel) every access stays inside the chunk.  Grouping never
+// group_span_kernel) every access stays inside the chunk.  Grouping never
 // affects results: deltas are diffs of the two boards, a refresh otherwise.
 __device__ __forceinline__ uint2 group_range(const uint2* __restrict__ span, uint32_t i, uint32_t n) {
   const uint2 v = span[i];
   return make_uint2(min(v.x, i), min(max(v.y, i + 1), n));
 }
 
-// Offsets of a call the host did not read (fnnue_eval_groups_device with
-// npos <= the workspace): non-decreasing, off[0] = 0, off[ngroups] = npos,
-// else error bit 2 (FNNUE_E_ARG).
-__global__ __launch_bounds__(256) void groups_check_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                           uint32_t npos, uint32_t* __restrict__ err) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngroups) return;
-  bool bad = off[g + 1] < off[g];
-  if (g == 0) bad |= off[0] != 0 || off[ngroups] != npos;
-  if (bad) atomicOr(err, 2u);
-}
-
 __device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int ksq, int kb) {
   return 16u * (uint32_t)(make_index(persp, s, pc, ksq) - kRowsPerBlock * kb);
 }
 
-__global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                                        const uint2* __restrict__ span, int star,
-                                                        uint32_t* __restrict__ ref,
-                                                        uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
-                                                        uint32_t* __restrict__ err) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// Refresh flags r0 / r1 and delta records of position i (both perspectives).
+__device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                              const uint2* __restrict__ span, int star, uint32_t* __restrict__ ref,
+                                              uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
+                                              uint32_t* __restrict__ err, uint32_t i, uint32_t& r0, uint32_t& r1) {
   const LaneBoard B = lane_decode(pos + i);
   if (!B.ok) {
     // no item, no accumulator; counted as a refresh so that STAR ranks skip it
     bucket[i] = 0xFF;
     ref[i] = ref[n + i] = 1;
+    r0 = r1 = 1;
     atomicOr(err, 1u);
     return;
   }
@@ -136,6 +143,7 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
       refresh = nr > 2 || na > 2;  // never for a legal move; arbitrary groups refresh
     }
     ref[c * n + i] = refresh ? 1u : 0u;
+    (c ? r1 : r0) = refresh ? 1u : 0u;
     if (!refresh) {
       const uint32_t half = B.stm == c ? 0u : 1u;
       dtmp[c * n + i] = make_uint4((2u * i + half) | bk << 25, rem[0] | rem[1] << 16, add[0] | add[1] << 16, 0u);
@@ -143,6 +151,75 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
   }
 }
 
+__global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+                                                        const uint2* __restrict__ span, int star,
+                                                        uint32_t* __restrict__ ref,
+                                                        uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
+                                                        uint32_t* __restrict__ err, uint32_t* __restrict__ bsum) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t r0 = 0, r1 = 0;
+  if (i < n) seg_delta_one(pos, n, span, star, ref, dtmp, bucket, err, i, r0, r1);
+#ifndef CUB_SCAN
+  // refresh counts of this block's 256 positions, per perspective (seg_scan_blocks)
+  const int c0 = __syncthreads_count((int)r0), c1 = __syncthreads_count((int)r1);
+  if (threadIdx.x == 0) {
+    bsum[blockIdx.x] = (uint32_t)c0;
+    bsum[gridDim.x + blockIdx.x] = (uint32_t)c1;
+  }
+#endif
+}
+
+// Exclusive scan of the per-block refresh counts (2 * nb of them, perspective
+// 0's blocks first, as ref is laid out) into block offsets, and cref[2n] =
+// the item count.  One workgroup; nb <= kMaxScanBlocks.
+constexpr uint32_t kMaxScanBlocks = 8192;
+__global__ __launch_bounds__(1024) void seg_scan_blocks_kernel(uint32_t* __restrict__ bsum, uint32_t nb, uint32_t n,
+                                                               uint32_t* __restrict__ cref) {
+  __shared__ uint32_t part[1024];
+  const uint32_t m = 2 * nb, per = (m + 1023) / 1024, t = threadIdx.x;
+  uint32_t sum = 0;
+  for (uint32_t k = 0; k < per; ++k) sum += t * per + k < m ? bsum[t * per + k] : 0u;
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t k = 0; k < per; ++k)
+    if (t * per + k < m) {
+      const uint32_t v = bsum[t * per + k];
+      bsum[t * per + k] = run;
+      run += v;
+    }
+  if (t == 1023) cref[2 * n] = part[1023];
+}
+
+// cref[j] (exclusive scan of ref) from the block offsets and a block-local
+// scan; item k = cref[j] of each refresh j gets its position (ipos).
+// Grid (nb, 2): block (b, c) covers positions 256 b .. +255 of perspective c.
+__global__ __launch_bounds__(256) void seg_items_scan_kernel(uint32_t n, const uint32_t* __restrict__ ref,
+                                                             const uint32_t* __restrict__ boff,
+                                                             uint32_t* __restrict__ cref, uint32_t* __restrict__ ipos) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y, j = c * n + i;
+  const uint32_t r = i < n ? ref[j] : 0u;
+  const uint64_t bal = __ballot(r != 0);
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t below = (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+  if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+  __syncthreads();
+  uint32_t base = boff[c * gridDim.x + blockIdx.x];
+  for (uint32_t w = 0; w < wv; ++w) base += wsum[w];
+  if (i >= n) return;
+  const uint32_t k = base + below;
+  cref[j] = k;
+  if (r) ipos[k] = i;
+}
+
+#ifdef CUB_SCAN
 // cref = exclusive scan of ref[0 .. 2n): refresh (c, i) is item cref[c*n+i]
 // (invalid positions count as refreshes without an item).
 __global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint32_t* __restrict__ ref,
@@ -151,44 +228,43 @@ __global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint32
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < 2 * n && ref[j]) ipos[cref[j]] = j % n;
 }
+#endif
 
-// Segment length at each valid refresh (0 elsewhere).  CHAIN: up to the next
-// refresh of the same perspective (the next item; groups start with one).
-// STAR: the group's parent owns its children that are not refreshes.
-__global__ __launch_bounds__(256) void seg_len_kernel(uint32_t n, const uint2* __restrict__ span, int star,
-                                                      const uint8_t* __restrict__ bucket,
-                                                      const uint32_t* __restrict__ ref,
-                                                      const uint32_t* __restrict__ cref,
-                                                      const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= 2 * n) return;
-  const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
-  uint32_t L = 0;
-  if (ref[j] && bucket[i] != 0xFF) {
-    if (star) {
-      const uint2 g = group_range(span, i, n);
-      L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
-    } else {
-      const uint32_t k = cref[j];
-      L = (k + 1 < cref[(c + 1) * n] ? ipos[k + 1] : n) - i;
-    }
-  }
-  len[j] = L;
-}
-
-__global__ __launch_bounds__(256) void seg_members_kernel(uint32_t n, const uint2* __restrict__ span, int star,
-                                                          const uint8_t* __restrict__ bucket,
-                                                          const uint32_t* __restrict__ ref,
-                                                          const uint32_t* __restrict__ cref,
-                                                          const uint32_t* __restrict__ ipos,
-                                                          const uint4* __restrict__ dtmp, uint4* __restrict__ drec) {
+// One thread per (perspective, position) j, after the scan and seg_items:
+// * a valid refresh gets its segment length (0 at every other j).  CHAIN: up
+//   to the next refresh of the same perspective (the next item; groups start
+//   with one).  STAR: the group's parent owns its children that are not
+//   refreshes.
+// * any other position places its delta record at root + rank, so that a
+//   segment's records are contiguous.
+__global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, int star,
+                                                        const uint8_t* __restrict__ bucket,
+                                                        const uint32_t* __restrict__ ref,
+                                                        const uint32_t* __restrict__ cref,
+                                                        const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len,
+                                                        const uint4* __restrict__ dtmp, uint4* __restrict__ drec) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   // Record 2n, read by items past the end of their segment: no rows, x row 2n
   // and bucket 0, i.e. x and PSQT stores just past the launch's buffer ranges
   // (dropped by the hardware), so the walk needs no liveness masking.
   if (j == 0) drec[2 * n] = make_uint4(2 * n, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
-  if (j >= 2 * n || ref[j]) return;
+  if (j >= 2 * n) return;
   const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+  if (ref[j]) {
+    uint32_t L = 0;
+    if (bucket[i] != 0xFF) {
+      if (star) {
+        const uint2 g = group_range(span, i, n);
+        L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
+      } else {
+        const uint32_t k = cref[j];
+        L = (k + 1 < cref[(c + 1) * n] ? ipos[k + 1] : n) - i;
+      }
+    }
+    len[j] = L;
+    return;
+  }
+  len[j] = 0;
   uint32_t r, rank;
   if (star) {
     r = group_range(span, i, n).x;  // the parent: a refresh item of this perspective
@@ -583,7 +659,7 @@ size_t seg_scan_temp_bytes(uint32_t chunk) {
   size_t b = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                          (int)(2 * chunk + 1));
-  return b;
+  return std::max(b, (size_t)8 * ((chunk + 255) / 256 + 1));  // or the block sums of seg_delta
 }
 
 #define FNNUE_HD_DISPATCH(hd, CALL) \
@@ -599,40 +675,37 @@ size_t seg_scan_temp_bytes(uint32_t chunk) {
     default: return hipErrorInvalidValue; \
   }
 
-hipError_t launch_groups_check(const uint32_t* off, uint32_t ngroups, uint32_t npos, uint32_t* err,
-                               hipStream_t stream) {
-  if (ngroups == 0) return hipSuccess;
-  hipLaunchKernelGGL(groups_check_kernel, dim3((ngroups + 255) / 256), dim3(256), 0, stream, off, ngroups, npos, err);
-  return hipGetLastError();
-}
-
 hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
                               uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
-                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid) {
-  if (n == 0) return hipSuccess;
+                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid,
+                              bool check_offsets) {
+  if (n == 0 && !check_offsets) return hipSuccess;
   const bool star = mode == FNNUE_GROUP_STAR;
-  hipError_t e = hipMemsetAsync(P.ctr, 0, sliced_ctr_words() * sizeof(uint32_t), stream);
-  if (e != hipSuccess) return e;
-  // ref[2n] is followed by one zero word so the scan yields cref[2n] = item count
-  if ((e = hipMemsetAsync(G.ref + 2 * (size_t)n, 0, 4, stream)) != hipSuccess) return e;
+  hipError_t e;
   const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
   const uint2* span = reinterpret_cast<const uint2*>(G.span);
-  hipLaunchKernelGGL(group_span_kernel, dim3((ngroups + 3) / 4), dim3(256), 0, stream, off, ngroups, base, n,
-                     (uint2*)G.span);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(group_span_kernel, dim3(max((ngroups + 3) / 4, 1u)), dim3(256), 0, stream, off, ngroups, base, n,
+                     (uint2*)G.span, P.ctr, (uint32_t)sliced_ctr_words(), G.ref, check_offsets ? 1 : 0, err);
+  if ((e = hipGetLastError()) != hipSuccess || n == 0) return e;
+  uint32_t* bsum = static_cast<uint32_t*>(G.scan_temp);
   hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, span, star ? 1 : 0, G.ref,
-                     (uint4*)G.dtmp, bucket, err);
+                     (uint4*)G.dtmp, bucket, err, bsum);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+#ifdef CUB_SCAN
   size_t tb = G.scan_temp_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(G.scan_temp, tb, G.ref, G.cref, (int)(2 * n + 1), stream)) != hipSuccess)
     return e;
   hipLaunchKernelGGL(seg_items_kernel, dim3(g2), dim3(bs), 0, stream, n, G.ref, G.cref, G.ipos);
+#else
+  // cref = exclusive scan of ref (reduce in seg_delta, scan of the block sums, local scans)
+  if (g1 > kMaxScanBlocks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(seg_scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, bsum, g1, n, G.cref);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_len_kernel, dim3(g2), dim3(bs), 0, stream, n, span, star ? 1 : 0, bucket,
-                     G.ref, G.cref, G.ipos, G.len);
+  hipLaunchKernelGGL(seg_items_scan_kernel, dim3(g1, 2), dim3(256), 0, stream, n, G.ref, bsum, G.cref, G.ipos);
+#endif
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_members_kernel, dim3(g2), dim3(bs), 0, stream, n, span, star ? 1 : 0, bucket,
-                     G.ref, G.cref, G.ipos, (const uint4*)G.dtmp, (uint4*)G.drec);
+  hipLaunchKernelGGL(seg_place_kernel, dim3(g2), dim3(bs), 0, stream, n, span, star ? 1 : 0, bucket, G.ref, G.cref,
+                     G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   uint32_t cb = (2 * n + 1023) / 1024;
   if (cb > 256) cb = 256;

@@ -110,12 +110,10 @@ uint32_t seg_max_units(uint32_t chunk);  // unit-table entries ft_segments may n
 hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
                               uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
                               uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream,
-                              hipEvent_t mid = nullptr);
-
-// Device-side check of group offsets (non-decreasing, spanning [0, npos)):
-// latches error bit 2 (FNNUE_E_ARG).  ft_segments stays in bounds regardless.
-hipError_t launch_groups_check(const uint32_t* off, uint32_t ngroups, uint32_t npos, uint32_t* err,
-                               hipStream_t stream);
+                              hipEvent_t mid = nullptr, bool check_offsets = false);
+// check_offsets: the offsets are also checked on the device (non-decreasing,
+// spanning [0, n)), latching error bit 2 (FNNUE_E_ARG); ft_segments stays in
+// bounds regardless.
 
 // MFMA operand-layout self test: returns number of mismatching outputs in *bad.
 hipError_t run_mfma_selftest(int* bad);
