@@ -260,6 +260,23 @@ def test_groups_of_unrelated_positions(ev_cache):
         assert np.array_equal(ps, ops) and np.array_equal(po, opo)
 
 
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 511, 513, 1025, 4097])
+def test_groups_ragged_sizes(ev_cache, n):
+    """Batch sizes around the segment plan's 256-position scan blocks (refresh
+    counts per block, block scan, local scans): CHAIN plies and STAR children,
+    the last group cut short."""
+    ev, on = ev_cache()
+    for mode, pm, count in ((N.GROUP_CHAIN, N.PLAYOUT_PLIES, 80), (N.GROUP_STAR, N.PLAYOUT_CHILDREN, 4)):
+        pos, off = F.random_playouts(31, count, mode=pm, threads=8)
+        assert len(pos) >= n
+        pos = pos[:n]
+        off = np.concatenate([off[off < n], [n]]).astype(np.uint32)
+        ps, po = ev.eval_groups(pos, off, mode)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert rc == 0
+        assert np.array_equal(ps, ops) and np.array_equal(po, opo)
+
+
 def test_groups_with_invalid_position(ev_cache):
     """An invalid position fails the batch (host API) and never feeds a delta."""
     ev, on = ev_cache()

@@ -201,3 +201,22 @@ def test_cpu_baseline_simd_invalid_positions():
     a = on.eval_packed(pos)
     assert rc != 0 and a[2] != 0
     assert np.array_equal(ps, a[0]) and np.array_equal(po, a[1])
+
+
+def test_later_sf_transform_equals_sfnnv5_transform():
+    """later Stockfish stores the FT weights and biases doubled
+    in memory and transforms with clamp(2a, 0, 254) * clamp(2b, 0, 254) >> 9;
+    SFNNv5 (this evaluator, the oracle) uses clamp(a, 0, 127) * clamp(b, 0, 127)
+    >> 7.  Exhaustive over every int16 accumulator pair whose doubled value
+    does not wrap (|a|, |b| < 2^14): the two transforms agree everywhere, so a
+    later net evaluates identically here whenever upstream's own doubled int16
+    accumulators do not wrap."""
+    a = np.arange(-(1 << 14), 1 << 14, dtype=np.int64)
+    # the clamp identity per operand, over the whole non-wrapping range
+    assert np.array_equal(np.clip(2 * a, 0, 254), 2 * np.clip(a, 0, 127))
+    # and the product/shift identity over every pair of clamped values
+    x = np.arange(128, dtype=np.int64)
+    later = (np.clip(2 * x, 0, 254)[:, None] * np.clip(2 * x, 0, 254)[None, :]) >> 9
+    v5 = (x[:, None] * x[None, :]) >> 7
+    assert np.array_equal(later, v5)
+    assert v5.max() == 126  # the u8 L1 input range both versions feed to fc_0
