@@ -67,7 +67,9 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic"], default="positions")
     ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions / variant workloads)")
-    ap.add_argument("--games", type=int, default=10_000, help="games per GPU (games / children workloads)")
+    ap.add_argument("--games", type=int, default=None,
+                    help="games per GPU (games: 10,000 = config 3; children: 5,000 ~ 12.5M positions per GPU = "
+                         "config 4's 1e8 positions over 8 GPUs)")
     ap.add_argument("--hd", type=int, default=1024)
     ap.add_argument("--small-net", type=int, default=0, metavar="HD",
                     help="also evaluate every position with a second (small) net of this width each step "
@@ -217,6 +219,8 @@ def make_inputs(F, args, seed, threads):
 
 def main():
     args = parse_args()
+    if args.games is None:
+        args.games = 5_000 if args.workload == "children" else 10_000
     import torch
     import torch.distributed as dist
 
@@ -332,7 +336,8 @@ def main():
         outs = [(s.psqt, s.positional) if k == 0 else (s.small[0], s.small[1]) for s in shards]
         if variant is not None and launch == "devices":
             multi.eval_vpositions_device([s.pos.data_ptr() for s in shards], [s.n for s in shards],
-                                         [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs])
+                                         [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs],
+                                         streams)
         elif variant is not None:
             s, e = shards[0], evs[k][0]
             e.eval_vpositions_device(s.pos.data_ptr(), s.n, outs[0][0].data_ptr(), outs[0][1].data_ptr(),
@@ -341,11 +346,11 @@ def main():
             m = multi if k == 0 else multi_small
             if not groups:
                 m.eval_positions_device([s.pos.data_ptr() for s in shards], [s.n for s in shards],
-                                        [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs])
+                                        [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs], streams)
             else:
                 m.eval_groups_device([s.pos.data_ptr() for s in shards], [s.off.data_ptr() for s in shards],
                                      [s.ng for s in shards], [s.n for s in shards], gmode,
-                                     [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs])
+                                     [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs], streams)
         else:
             s, e = shards[0], evs[k][0]
             stream = torch.cuda.current_stream().cuda_stream
@@ -354,6 +359,10 @@ def main():
             else:
                 e.eval_groups_device(s.pos.data_ptr(), s.off.data_ptr(), s.ng, s.n, gmode, outs[0][0].data_ptr(),
                                      outs[0][1].data_ptr(), stream)
+
+    # every device's work on torch's current stream of that device (after the
+    # input copies); one process launch: no host sync between devices
+    streams = [torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream for d in devices]
 
     def step():
         for k in range(len(evs)):
@@ -420,7 +429,26 @@ def main():
         gms = (time.perf_counter() - tg) * 1e3
         if rank == 0:
             gathered = {"positions": int(g_ps.size), "gather_ms": round(gms, 3),
-                        "equals_sum_of_shards": bool(g_ps.size == g_po.size == int(total_positions))}
+                        "equals_sum_of_shards": bool(g_ps.size == g_po.size == int(total_positions)),
+                        "how": "torch.distributed gather to rank 0 over RCCL"}
+    else:
+        # one process: every device's results D2H into disjoint slices of one
+        # pinned host buffer per output (the per-rank gather of SURVEY §8e)
+        sync_all()
+        tg = time.perf_counter()
+        h_ps = torch.empty(int(total_positions), dtype=torch.int32, pin_memory=True)
+        h_po = torch.empty(int(total_positions), dtype=torch.int32, pin_memory=True)
+        lo = 0
+        for s in shards:
+            h_ps[lo:lo + s.n].copy_(s.psqt, non_blocking=True)
+            h_po[lo:lo + s.n].copy_(s.positional, non_blocking=True)
+            lo += s.n
+        sync_all()
+        gms = (time.perf_counter() - tg) * 1e3
+        gathered = {"positions": lo, "gather_ms": round(gms, 3),
+                    "equals_sum_of_shards": bool(lo == int(total_positions)
+                                                 and np.array_equal(h_ps[:npos].numpy(), psqt)),
+                    "how": "one process: D2H of every device's shard into disjoint slices of pinned host buffers"}
     small = None
     if args.small_net and rank == 0:
         # parity of the small net on a bounded sample against the oracle (test infrastructure)
@@ -436,7 +464,9 @@ def main():
                                        if rc2 == 0 else None}}
 
     cpu, parity = None, None
-    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and variant is not None:
+    # The CPU baseline at every N (rank 0 / device 0's shard, same host cores):
+    # it doubles as the parity spot check of that shard.
+    if rank == 0 and not args.no_cpu_baseline and variant is not None:
         from oracle.oracle import VariantOracleNet  # cpu_baseline leg: the scalar C restatement is the CPU port
         on = VariantOracleNet(F.synthesize_variant_net(args.seed, args.hd, variant), variant)
         done, mism, t0 = 0, 0, time.perf_counter()
@@ -456,7 +486,7 @@ def main():
                          f"wall on {threads} threads; oracle/variant_oracle.c = scalar C restatement of "
                          f"Fairy-Stockfish's HalfKAv2-variants NNUE, -O3, no SIMD: Fairy-Stockfish itself is absent)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
-    elif rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+    elif rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import OracleNet  # cpu_baseline leg: oracle/nnue_cpu_simd.c is the timed CPU port
         from oracle.oracle import lib as olib
         isa = "AVX-512 VNNI" if olib.cpu_simd_isa512() else "AVX2"
@@ -493,13 +523,13 @@ def main():
                          f"NNUE code paths restated (register-tiled accumulators, maddubs/VPDPBUSD affine), -O3; "
                          f"bit-identical to the scalar oracle)"}
         parity = {"checked": min(done, npos), "mismatches": mism}
-    elif rank == 0 and launch == "devices" and variant is not None:
+    elif rank == 0 and variant is not None:
         from oracle.oracle import VariantOracleNet
         on = VariantOracleNet(F.synthesize_variant_net(args.seed, args.hd, variant), variant)
         k = min(npos, 50_000)
         ops, opo, rc = on.eval_packed(pos[:k], threads=threads)
         parity = {"checked": k, "mismatches": int(((ops != psqt[:k]) | (opo != positional[:k])).sum())}
-    elif rank == 0 and launch == "devices":
+    elif rank == 0:
         # spot check of device 0's shard against the oracle (test infrastructure)
         from oracle.oracle import OracleNet
         on = OracleNet(F.synthesize_net(args.seed, args.hd, 0))

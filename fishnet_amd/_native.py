@@ -100,11 +100,12 @@ SIGNATURES = {
     "fnnue_multi_ctx": ([_vp, _i32, _P(_vp)], _i32),
     "fnnue_multi_eval_positions": ([_vp, _vp, _sz, _vp, _vp], _i32),
     "fnnue_multi_eval_groups": ([_vp, _vp, _sz, _vp, _sz, _i32, _vp, _vp], _i32),
-    "fnnue_multi_eval_positions_device": ([_vp, _P(_vp), _P(_sz), _P(_vp), _P(_vp)], _i32),
-    "fnnue_multi_eval_groups_device": ([_vp, _P(_vp), _P(_vp), _P(_sz), _P(_sz), _i32, _P(_vp), _P(_vp)], _i32),
+    "fnnue_multi_eval_positions_device": ([_vp, _P(_vp), _P(_sz), _P(_vp), _P(_vp), _P(_vp)], _i32),
+    "fnnue_multi_eval_groups_device": ([_vp, _P(_vp), _P(_vp), _P(_sz), _P(_sz), _i32, _P(_vp), _P(_vp), _P(_vp)],
+                                       _i32),
     "fnnue_multi_sync": ([_vp], _i32),
     "fnnue_multi_eval_vpositions": ([_vp, _vp, _sz, _vp, _vp], _i32),
-    "fnnue_multi_eval_vpositions_device": ([_vp, _P(_vp), _P(_sz), _P(_vp), _P(_vp)], _i32),
+    "fnnue_multi_eval_vpositions_device": ([_vp, _P(_vp), _P(_sz), _P(_vp), _P(_vp), _P(_vp)], _i32),
     "fnnue_partition_groups": ([_vp, _sz, _i32, _vp], _i32),
     "fnnue_net_load_variant": ([C.c_char_p, _i32, _P(_vp)], _i32),
     "fnnue_net_load_variant_mem": ([_vp, _sz, _i32, _P(_vp)], _i32),

@@ -104,10 +104,6 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant) {
   c->variant = variant;
   c->nfeat = features_of(variant);
   c->chunk = chunk_for_hd(hd);
-  if (const char* s = std::getenv("FNNUE_CHUNK")) {  // experiment knob: smaller launches (multiple of 1024)
-    const unsigned long v = std::strtoul(s, nullptr, 10) & ~1023ul;
-    if (v >= 1024 && v < c->chunk) c->chunk = (uint32_t)v;
-  }
   const uint32_t chunk = c->chunk;
   DeviceGuard g(device);
   c->image_bytes = image_layout(hd, c->nfeat).total;
@@ -262,9 +258,24 @@ int ensure_seg(fnnue_ctx* c) {
   if (hipMalloc(&G.ref, (n2 + 1) * 4) != hipSuccess || hipMalloc(&G.cref, (n2 + 1) * 4) != hipSuccess ||
       hipMalloc(&G.dtmp, n2 * 16) != hipSuccess || hipMalloc(&G.drec, n2 * 16 + 16) != hipSuccess ||
       hipMalloc(&G.ipos, n2 * 4) != hipSuccess || hipMalloc(&G.len, n2 * 4) != hipSuccess ||
-      hipMalloc(&G.items, n2 * 16) != hipSuccess || hipMalloc(&G.span, (size_t)c->chunk * 8) != hipSuccess ||
-      hipMalloc(&G.scan_temp, G.scan_temp_bytes + 16) != hipSuccess)
+      hipMalloc(&G.items, n2 * 16) != hipSuccess || hipMalloc(&G.scan_temp, G.scan_temp_bytes + 16) != hipSuccess)
     return fail(FNNUE_E_OOM, "device allocation (segment plan)");
+  return FNNUE_OK;
+}
+
+// The per-position group span table of a grouped call (8 B per position of
+// the call, grow-only: a call above the workspace keeps its whole span table
+// in HBM instead of reading its offsets on the host).  Growing frees the old
+// table, which hipFree orders after the device's pending work.
+int ensure_span(fnnue_ctx* c, size_t npos) {
+  SegPlan& G = c->seg;
+  const size_t want = std::max<size_t>(npos, c->chunk);
+  if (G.span && G.span_cap >= want) return FNNUE_OK;
+  if (G.span) (void)hipFree(G.span);
+  G.span = nullptr;
+  G.span_cap = 0;
+  if (hipMalloc(&G.span, want * 8) != hipSuccess) return fail(FNNUE_E_OOM, "device allocation (group spans)");
+  G.span_cap = want;
   return FNNUE_OK;
 }
 
@@ -278,14 +289,22 @@ int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t 
   return FNNUE_OK;
 }
 
-// Orders this call's workspace use after the previous call's when the two
-// run on different streams (the workspace is shared by all calls on a ctx).
-int order_workspace(fnnue_ctx* c, hipStream_t s) {
-  if (c->last_stream && c->last_stream != s) {
-    HIP_TRY(hipEventRecord(c->ws_event, c->last_stream), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(s, c->ws_event, 0), "hipStreamWaitEvent");
+// Workspace ordering across streams (the workspace is shared by every call on
+// a ctx): each *_device call first waits for the event the previous call
+// recorded on its own stream, and records the event on its stream when its
+// work is enqueued (also after an error: part of it may be).  No stream handle
+// of an earlier call is ever used again, so a caller may destroy a stream
+// right after a call on it.
+struct WorkspaceUse {
+  fnnue_ctx* c;
+  hipStream_t s;
+  ~WorkspaceUse() {
+    if (hipEventRecord(c->ws_event, s) == hipSuccess) c->ws_recorded = true;
   }
-  c->last_stream = s;
+};
+
+int order_workspace(fnnue_ctx* c, hipStream_t s) {
+  if (c->ws_recorded) HIP_TRY(hipStreamWaitEvent(s, c->ws_event, 0), "hipStreamWaitEvent");
   return FNNUE_OK;
 }
 
@@ -296,7 +315,7 @@ hipEvent_t mid_event(std::array<hipEvent_t, 4>* ev) { return ev ? (*ev)[1] : nul
 extern "C" {
 
 const char* fnnue_last_error(void) { return g_err.c_str(); }
-uint32_t fnnue_abi_version(void) { return (2u << 16) | 0u; }
+uint32_t fnnue_abi_version(void) { return (3u << 16) | 0u; }
 
 int fnnue_net_load_mem(const void* buf, size_t len, fnnue_net** out) {
   if (!buf || !out) return fail(FNNUE_E_ARG, "null argument");
@@ -565,6 +584,7 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   int rc = order_workspace(ctx, s);
   if (rc) return rc;
+  WorkspaceUse use{ctx, s};
   for (size_t b = 0; b < n; b += ctx->chunk) {
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
@@ -592,63 +612,47 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
 
 int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint32_t* d_off, size_t ngroups,
                              size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {
-  // d_off is device memory; the chunking needs the group boundaries on the
-  // host, so this entry point copies them once (ngroups+1 words).
+  // The offsets stay on the device (no D2H, no stream drain, at any size): they
+  // are checked there (group_span_kernel, latched as FNNUE_E_ARG), and a call
+  // above one workspace is cut into chunks at fixed positions; a group cut by
+  // a chunk boundary restarts there with a refresh (results are identical).
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
-  if (ctx->variant != kVariantChess) return fail(FNNUE_E_ARCH, "variant net: use fnnue_eval_vgroups*");
+  if (ctx->variant != kVariantChess)
+    return fail(FNNUE_E_ARCH, "variant net: grouped evaluation is not supported for variant nets; use "
+                              "fnnue_eval_vpositions*");
   if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
-  if (ngroups == 0) return FNNUE_OK;
+  if (ngroups == 0) return npos == 0 ? FNNUE_OK : fail(FNNUE_E_ARG, "positions without groups");
+  if (ngroups > 0xFFFFFFFFu || npos > 0xFFFFFFFFu) return fail(FNNUE_E_ARG, "batch too large");
   if (!d_pos || !d_off || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null buffer");
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-  if (int rc = order_workspace(ctx, s)) return rc;
-  if (ctx->ft_impl == FNNUE_FT_SLICED) {
-    int rc = ensure_seg(ctx);
-    if (rc) return rc;
-    if (npos <= ctx->chunk) {
-      // One launch: the offsets never come to the host (no D2H round trip and
-      // no stream drain per call); they are checked on the device instead.
-      std::array<hipEvent_t, 4>* ev = nullptr;
-      if ((rc = next_events(ctx, &ev))) return rc;
-      if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
-      HIP_TRY(launch_ft_segments(ctx->hd, d_pos, (uint32_t)npos, d_off, (uint32_t)ngroups, 0, mode, ctx->ptrs,
-                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev),
-                                 /*check_offsets=*/true),
-              "ft_segments launch");
-      return run_chunk_tail(ctx, (uint32_t)npos, d_positional, s, ev, nullptr, ctx->plan.psqt_part, d_psqt);
-    }
-  }
-  std::vector<uint32_t> off(ngroups + 1);
-  HIP_TRY(hipMemcpyAsync(off.data(), d_off, off.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "hipMemcpy");
-  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-  if (off[0] != 0 || off[ngroups] != npos) return fail(FNNUE_E_ARG, "group offsets must span [0, npos)");
-  size_t gb = 0;
-  while (gb < ngroups) {
-    size_t ge = gb;
-    while (ge < ngroups && off[ge + 1] - off[gb] <= ctx->chunk) {
-      if (off[ge + 1] < off[ge]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
-      ++ge;
-    }
-    if (ge == gb) return fail(FNNUE_E_ARG, "a group is larger than the device workspace");
-    const uint32_t base = off[gb], m = off[ge] - off[gb];
+  int rc = order_workspace(ctx, s);
+  if (rc) return rc;
+  WorkspaceUse use{ctx, s};
+  const bool sliced = ctx->ft_impl == FNNUE_FT_SLICED;
+  if (sliced && ((rc = ensure_seg(ctx)) || (rc = ensure_span(ctx, npos)))) return rc;
+  HIP_TRY(launch_group_span(d_off, (uint32_t)ngroups, (uint32_t)npos, sliced ? ctx->seg.span : nullptr, true,
+                            ctx->err, s),
+          "group_span launch");
+  const uint2* span = static_cast<const uint2*>(ctx->seg.span);
+  for (size_t b = 0; b < npos; b += ctx->chunk) {
+    const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, npos - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
-    int rc = next_events(ctx, &ev);
-    if (rc) return rc;
+    if ((rc = next_events(ctx, &ev))) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
-    if (ctx->ft_impl == FNNUE_FT_SLICED) {
-      HIP_TRY(launch_ft_segments(ctx->hd, d_pos + base, m, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs,
-                                 ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
+    if (sliced) {
+      HIP_TRY(launch_ft_segments(ctx->hd, d_pos + b, m, span + b, (uint32_t)b, mode, ctx->ptrs, ctx->plan, ctx->seg,
+                                 ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
               "ft_segments launch");
-      rc = run_chunk_tail(ctx, m, d_positional + base, s, ev, nullptr, ctx->plan.psqt_part, d_psqt + base);
+      rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, nullptr, ctx->plan.psqt_part, d_psqt + b);
     } else {
       if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
-      HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off + gb, (uint32_t)(ge - gb), base, mode, ctx->ptrs, ctx->x,
-                               d_psqt + base, ctx->bucket, ctx->err, s),
+      HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off, (uint32_t)ngroups, (uint32_t)b, (uint32_t)(b + m), mode,
+                               ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_groups launch");
-      rc = run_chunk_tail(ctx, m, d_positional + base, s, ev);
+      rc = run_chunk_tail(ctx, m, d_positional + b, s, ev);
     }
     if (rc) return rc;
-    gb = ge;
   }
   return FNNUE_OK;
 }
@@ -663,6 +667,7 @@ int fnnue_eval_vpositions_device(fnnue_ctx* ctx, const fnnue_vpos* d_pos, size_t
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   int rc = order_workspace(ctx, s);
   if (rc) return rc;
+  WorkspaceUse use{ctx, s};
   for (size_t b = 0; b < n; b += ctx->chunk) {
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
@@ -729,7 +734,12 @@ int fnnue_eval_vpositions(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t n, int32
 int fnnue_ctx_check(fnnue_ctx* ctx) {
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
   DeviceGuard g(ctx->device);
-  HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  // Only this context's work: its own stream, and the last *_device call
+  // (whatever stream it ran on; calls are chained by ws_event, so the last
+  // one's completion implies every earlier one's).  Other streams of the
+  // device (other contexts, torch) are not drained.
+  HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+  if (ctx->ws_recorded) HIP_TRY(hipEventSynchronize(ctx->ws_event), "hipEventSynchronize");
   return latched(ctx);
 }
 

@@ -16,11 +16,15 @@
 // the previous accumulator (CHAIN) or to the parent's (STAR).  int16 add/sub
 // wrap is a group, so results equal a refresh bit for bit.
 //
-// Plan (all on the device, per chunk of positions):
-//   group_span    per position its group's {first, end} (wave per group);
-//                 zeroes the counters; checks device-only offsets
+// Plan (all on the device):
+//   group_span    once per call: per position its group's {first, end}
+//                 (wave per group); checks the device-only offsets
+// then per chunk of <= 2^20 positions (cut at fixed positions, not at group
+// boundaries, so no offset ever comes to the host; a group cut by a chunk
+// boundary restarts with a refresh there, group_range):
 //   seg_delta     per (position, perspective): refresh flag or the delta
-//                 record {slot, half, bucket, 2 removed, 2 added rows}
+//                 record {slot, half, bucket, 2 removed, 2 added rows};
+//                 zeroes the counters
 //   scan          exclusive scan of refresh flags -> item index per refresh:
 //                 block counts in seg_delta, seg_scan_blocks, then local
 //                 scans in seg_items_scan, which also maps item k -> its
@@ -37,7 +41,6 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
-#include <hipcub/hipcub.hpp>
 
 #include "sliced_common.h"
 
@@ -50,42 +53,40 @@ constexpr uint32_t kRowMask = 0x1FFFFFF;  // delta record x: (2 * slot + half) |
 // A segment item is a whole run of positions walked serially, so units are
 // cut by positions (kSegUnitPlies, plan_scan_kernel) rather than by items.
 
-// Each position's group span {first, end} (chunk-relative), written by
-// group_span_kernel: one wave per group fills its members (coalesced), so the
-// plan kernels read one word pair instead of binary-searching the offsets.
-// The first kernel of the plan, it also zeroes the counter block and the word
-// after ref[2n] (instead of two memset launches) and, with check set (offsets
-// the host never read: fnnue_eval_groups_device with npos <= the workspace),
-// checks them: non-decreasing, off[0] = 0, off[ngroups] = npos, else error
-// bit 2 (FNNUE_E_ARG).
+// Each position's group span {first, end}, absolute positions of the whole
+// call, written once per call by group_span_kernel (one wave per group fills
+// its members, coalesced) so the plan kernels of every chunk read one word
+// pair instead of binary-searching the offsets.  With check set it also checks
+// the offsets (non-decreasing, off[0] = 0, off[ngroups] = npos; else error bit
+// 2, FNNUE_E_ARG): the offsets of a *_device call never come to the host.
+// span == nullptr: check only (the gather path).
 __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                         uint32_t base, uint32_t n, uint2* __restrict__ span,
-                                                         uint32_t* __restrict__ ctr, uint32_t ctr_words,
-                                                         uint32_t* __restrict__ ref, int check,
+                                                         uint32_t npos, uint2* __restrict__ span, int check,
                                                          uint32_t* __restrict__ err) {
-  if (blockIdx.x == 0) {
-    for (uint32_t i = threadIdx.x; i < ctr_words; i += blockDim.x) ctr[i] = 0;
-    if (threadIdx.x == 0) ref[2 * n] = 0;  // the scan then yields cref[2n] = item count
-  }
   const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= ngroups) return;
   if (check && (threadIdx.x & 63) == 0) {
     bool bad = off[g + 1] < off[g];
-    if (g == 0) bad |= off[0] != 0 || off[ngroups] != n;
+    if (g == 0) bad |= off[0] != 0 || off[ngroups] != npos;
     if (bad) atomicOr(err, 2u);
   }
-  const uint32_t a = min(off[g] - base, n), b = min(max(off[g + 1] - base, a), n);
+  if (!span) return;
+  const uint32_t a = min(off[g], npos), b = min(max(off[g + 1], a), npos);
   for (uint32_t i = a + (threadIdx.x & 63); i < b; i += 64) span[i] = make_uint2(a, b);
 }
 
-// The group of position i, clamped to first <= i < end <= n.  With valid
-// offsets the clamp is a no-op; with malformed ones (gaps leave span entries
-// unwritten; the device entry point checks offsets on the device,
-// group_span_kernel) every access stays inside the chunk.  Grouping never
-// affects results: deltas are diffs of the two boards, a refresh otherwise.
-__device__ __forceinline__ uint2 group_range(const uint2* __restrict__ span, uint32_t i, uint32_t n) {
+// The group of chunk position i (absolute position sbase + i), in chunk
+// coordinates and clamped to first <= i < end <= n.  A group that starts
+// before the chunk starts at the chunk's first position there (its first
+// in-chunk position is refreshed: a CHAIN continues from it, a STAR's
+// remaining children derive from it); one that ends after the chunk ends at
+// the chunk's end.  With malformed offsets (gaps leave span entries
+// unwritten) every access stays inside the chunk.  Grouping never affects
+// results: deltas are diffs of the two boards, a refresh otherwise.
+__device__ __forceinline__ uint2 group_range(const uint2* __restrict__ span, uint32_t i, uint32_t n, uint32_t sbase) {
   const uint2 v = span[i];
-  return make_uint2(min(v.x, i), min(max(v.y, i + 1), n));
+  const uint32_t a = v.x > sbase ? v.x - sbase : 0u, b = v.y > sbase ? v.y - sbase : 0u;
+  return make_uint2(min(a, i), min(max(b, i + 1), n));
 }
 
 __device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int ksq, int kb) {
@@ -94,7 +95,8 @@ __device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int 
 
 // Refresh flags r0 / r1 and delta records of position i (both perspectives).
 __device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                              const uint2* __restrict__ span, int star, uint32_t* __restrict__ ref,
+                                              const uint2* __restrict__ span, uint32_t sbase, int star,
+                                              uint32_t* __restrict__ ref,
                                               uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
                                               uint32_t* __restrict__ err, uint32_t i, uint32_t& r0, uint32_t& r1) {
   const LaneBoard B = lane_decode(pos + i);
@@ -108,7 +110,7 @@ __device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos,
   }
   const uint32_t bk = (uint32_t)(B.cnt - 1) >> 2;
   bucket[i] = (uint8_t)bk;
-  const uint32_t first = group_range(span, i, n).x;
+  const uint32_t first = group_range(span, i, n, sbase).x;
   const bool has_base = i > first;
   LaneBoard A;
   bool base_ok = false;
@@ -151,22 +153,25 @@ __device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos,
   }
 }
 
+// The first kernel of a chunk's plan: block 0 also zeroes the counter block
+// (read by seg_count / plan_scan / seg_scatter) instead of a memset launch.
 __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
-                                                        const uint2* __restrict__ span, int star,
+                                                        const uint2* __restrict__ span, uint32_t sbase, int star,
                                                         uint32_t* __restrict__ ref,
                                                         uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
-                                                        uint32_t* __restrict__ err, uint32_t* __restrict__ bsum) {
+                                                        uint32_t* __restrict__ err, uint32_t* __restrict__ bsum,
+                                                        uint32_t* __restrict__ ctr, uint32_t ctr_words) {
+  if (blockIdx.x == 0)
+    for (uint32_t k = threadIdx.x; k < ctr_words; k += blockDim.x) ctr[k] = 0;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t r0 = 0, r1 = 0;
-  if (i < n) seg_delta_one(pos, n, span, star, ref, dtmp, bucket, err, i, r0, r1);
-#ifndef CUB_SCAN
+  if (i < n) seg_delta_one(pos, n, span, sbase, star, ref, dtmp, bucket, err, i, r0, r1);
   // refresh counts of this block's 256 positions, per perspective (seg_scan_blocks)
   const int c0 = __syncthreads_count((int)r0), c1 = __syncthreads_count((int)r1);
   if (threadIdx.x == 0) {
     bsum[blockIdx.x] = (uint32_t)c0;
     bsum[gridDim.x + blockIdx.x] = (uint32_t)c1;
   }
-#endif
 }
 
 // Exclusive scan of the per-block refresh counts (2 * nb of them, perspective
@@ -219,16 +224,6 @@ __global__ __launch_bounds__(256) void seg_items_scan_kernel(uint32_t n, const u
   if (r) ipos[k] = i;
 }
 
-#ifdef CUB_SCAN
-// cref = exclusive scan of ref[0 .. 2n): refresh (c, i) is item cref[c*n+i]
-// (invalid positions count as refreshes without an item).
-__global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint32_t* __restrict__ ref,
-                                                        const uint32_t* __restrict__ cref,
-                                                        uint32_t* __restrict__ ipos) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j < 2 * n && ref[j]) ipos[cref[j]] = j % n;
-}
-#endif
 
 // One thread per (perspective, position) j, after the scan and seg_items:
 // * a valid refresh gets its segment length (0 at every other j).  CHAIN: up
@@ -237,7 +232,8 @@ __global__ __launch_bounds__(256) void seg_items_kernel(uint32_t n, const uint32
 //   refreshes.
 // * any other position places its delta record at root + rank, so that a
 //   segment's records are contiguous.
-__global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, int star,
+__global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, uint32_t sbase,
+                                                        int star,
                                                         const uint8_t* __restrict__ bucket,
                                                         const uint32_t* __restrict__ ref,
                                                         const uint32_t* __restrict__ cref,
@@ -254,7 +250,7 @@ __global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2*
     uint32_t L = 0;
     if (bucket[i] != 0xFF) {
       if (star) {
-        const uint2 g = group_range(span, i, n);
+        const uint2 g = group_range(span, i, n, sbase);
         L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
       } else {
         const uint32_t k = cref[j];
@@ -267,7 +263,7 @@ __global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2*
   len[j] = 0;
   uint32_t r, rank;
   if (star) {
-    r = group_range(span, i, n).x;  // the parent: a refresh item of this perspective
+    r = group_range(span, i, n, sbase).x;  // the parent: a refresh item of this perspective
     rank = (i - r) - (cref[j] - cref[c * n + r + 1]);
   } else {
     r = ipos[cref[j] - 1];  // the last refresh of this perspective before i (same game)
@@ -466,10 +462,7 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   // then read records 144 B apart, 4 banks, instead of 128 B = the same banks.
   uint4* db = dbuf + kDbufStride * it_in_wave;
   const uint32_t nb = __builtin_amdgcn_readfirstlane((maxL - 1 + 7) / 8);  // batches, wave-uniform
-#ifndef SEG_PREFETCH
-#define SEG_PREFETCH 1
-#endif
-  constexpr int kAhead = SEG_PREFETCH;  // batches of records in flight ahead of the current one
+  constexpr int kAhead = 1;  // batches of records in flight ahead of the current one (2: no gain, r01)
   uint4 next[kAhead];
 #pragma unroll
   for (int a = 0; a < kAhead; ++a) next[a] = fetch(8 * a + 1 + q);
@@ -655,12 +648,8 @@ hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& n
 // a unit holding fewer than kSegUnitPlies / 160 items is its king block's last
 uint32_t seg_max_units(uint32_t chunk) { return 32 + (2 * chunk + kSegUnitPlies / 160 - 1) / (kSegUnitPlies / 160); }
 
-size_t seg_scan_temp_bytes(uint32_t chunk) {
-  size_t b = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                         (int)(2 * chunk + 1));
-  return std::max(b, (size_t)8 * ((chunk + 255) / 256 + 1));  // or the block sums of seg_delta
-}
+// the per-block refresh counts of seg_delta, two perspectives
+size_t seg_scan_temp_bytes(uint32_t chunk) { return (size_t)8 * ((chunk + 255) / 256 + 1); }
 
 #define FNNUE_HD_DISPATCH(hd, CALL) \
   switch (hd) {                     \
@@ -675,37 +664,34 @@ size_t seg_scan_temp_bytes(uint32_t chunk) {
     default: return hipErrorInvalidValue; \
   }
 
-hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
-                              uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
-                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid,
-                              bool check_offsets) {
-  if (n == 0 && !check_offsets) return hipSuccess;
+hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npos, void* span, bool check,
+                             uint32_t* err, hipStream_t stream) {
+  if (ngroups == 0) return hipSuccess;
+  hipLaunchKernelGGL(group_span_kernel, dim3((ngroups + 3) / 4), dim3(256), 0, stream, off, ngroups, npos,
+                     static_cast<uint2*>(span), check ? 1 : 0, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const void* span, uint32_t sbase,
+                              int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
+                              uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid) {
+  if (n == 0) return hipSuccess;
   const bool star = mode == FNNUE_GROUP_STAR;
   hipError_t e;
   const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
-  const uint2* span = reinterpret_cast<const uint2*>(G.span);
-  hipLaunchKernelGGL(group_span_kernel, dim3(max((ngroups + 3) / 4, 1u)), dim3(256), 0, stream, off, ngroups, base, n,
-                     (uint2*)G.span, P.ctr, (uint32_t)sliced_ctr_words(), G.ref, check_offsets ? 1 : 0, err);
-  if ((e = hipGetLastError()) != hipSuccess || n == 0) return e;
-  uint32_t* bsum = static_cast<uint32_t*>(G.scan_temp);
-  hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, span, star ? 1 : 0, G.ref,
-                     (uint4*)G.dtmp, bucket, err, bsum);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-#ifdef CUB_SCAN
-  size_t tb = G.scan_temp_bytes;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(G.scan_temp, tb, G.ref, G.cref, (int)(2 * n + 1), stream)) != hipSuccess)
-    return e;
-  hipLaunchKernelGGL(seg_items_kernel, dim3(g2), dim3(bs), 0, stream, n, G.ref, G.cref, G.ipos);
-#else
-  // cref = exclusive scan of ref (reduce in seg_delta, scan of the block sums, local scans)
   if (g1 > kMaxScanBlocks) return hipErrorInvalidValue;
+  const uint2* sp = static_cast<const uint2*>(span);
+  uint32_t* bsum = static_cast<uint32_t*>(G.scan_temp);
+  hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, sp, sbase, star ? 1 : 0, G.ref,
+                     (uint4*)G.dtmp, bucket, err, bsum, P.ctr, (uint32_t)sliced_ctr_words());
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // cref = exclusive scan of ref (reduce in seg_delta, scan of the block sums, local scans)
   hipLaunchKernelGGL(seg_scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, bsum, g1, n, G.cref);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(seg_items_scan_kernel, dim3(g1, 2), dim3(256), 0, stream, n, G.ref, bsum, G.cref, G.ipos);
-#endif
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_place_kernel, dim3(g2), dim3(bs), 0, stream, n, span, star ? 1 : 0, bucket, G.ref, G.cref,
-                     G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec);
+  hipLaunchKernelGGL(seg_place_kernel, dim3(g2), dim3(bs), 0, stream, n, sp, sbase, star ? 1 : 0, bucket, G.ref,
+                     G.cref, G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   uint32_t cb = (2 * n + 1023) / 1024;
   if (cb > 256) cb = 256;

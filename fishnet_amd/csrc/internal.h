@@ -47,10 +47,10 @@ struct fnnue_ctx {
   std::vector<std::array<hipEvent_t, 4>> evpool;
   size_t evused = 0;
   // Workspace ordering across streams: every *_device call writes the same
-  // workspace (x, bucket, plan, err); a call on a different stream than the
-  // previous one first waits for the previous one's work (ws_event).
-  hipStream_t last_stream = nullptr;
+  // workspace (x, bucket, plan, err); it waits for ws_event (recorded by the
+  // previous call on its stream) and records ws_event on its own stream.
   hipEvent_t ws_event = nullptr;
+  bool ws_recorded = false;
 };
 
 

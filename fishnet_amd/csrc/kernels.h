@@ -27,9 +27,12 @@ hipError_t launch_ft_scratch(uint32_t hd, const fnnue_pos* pos, uint32_t n, cons
 
 // Feature transformer along groups (CHAIN: incremental along plies; STAR:
 // children derived from the group's first position).  One wave per group.
+// Positions [lo, hi) of the call (a chunk): every group is clamped to it, a
+// group cut at lo restarting there with a refresh; x / psqt / bucket are
+// chunk-relative (row i - lo).
 hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups,
-                            uint32_t base, int mode, const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket,
-                            uint32_t* err, hipStream_t stream);
+                            uint32_t lo, uint32_t hi, int mode, const NetPtrs& net, uint8_t* x, int32_t* psqt,
+                            uint8_t* bucket, uint32_t* err, hipStream_t stream);
 
 // Layer stacks: 16 positions per wave, int8 MFMA for fc_0 and fc_1.  Row i of
 // x / bucket is written to positional[perm ? perm[i] : i]; when psqt_part is
@@ -101,19 +104,25 @@ struct SegPlan {
   uint32_t* ipos;     // [2 * chunk] item -> root position
   uint32_t* len;      // [2 * chunk] segment length at the root
   void* items;        // uint4 [2 * chunk] sorted item records
-  void* span;         // uint2 [chunk] group {first, end} per position
+  void* span;         // uint2 [span_cap] group {first, end} per position of a call (grow-only)
+  size_t span_cap;
   void* scan_temp;
   size_t scan_temp_bytes;
 };
 size_t seg_scan_temp_bytes(uint32_t chunk);
 uint32_t seg_max_units(uint32_t chunk);  // unit-table entries ft_segments may need
-hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
-                              uint32_t base, int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G,
-                              uint8_t* x, uint8_t* bucket, uint32_t* err, hipStream_t stream,
-                              hipEvent_t mid = nullptr, bool check_offsets = false);
-// check_offsets: the offsets are also checked on the device (non-decreasing,
-// spanning [0, n)), latching error bit 2 (FNNUE_E_ARG); ft_segments stays in
-// bounds regardless.
+// Once per grouped call: span[i] = {first, end} of position i's group
+// (absolute, npos entries; span == nullptr: check only).  check: the offsets
+// are checked on the device (non-decreasing, spanning [0, npos)), latching
+// error bit 2 (FNNUE_E_ARG); every kernel stays in bounds regardless.
+hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npos, void* span, bool check,
+                             uint32_t* err, hipStream_t stream);
+// One chunk: positions pos[0, n) = the call's positions [sbase, sbase + n),
+// span = the call's span table + sbase.  Groups cut by the chunk's edges are
+// clamped to it (their first in-chunk position refreshes).
+hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const void* span, uint32_t sbase,
+                              int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
+                              uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid = nullptr);
 
 // MFMA operand-layout self test: returns number of mismatching outputs in *bad.
 hipError_t run_mfma_selftest(int* bad);

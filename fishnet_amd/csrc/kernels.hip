@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void ft_scratch_kernel(const fnnue_pos* __rest
 template <int HD, int U>
 __global__ __launch_bounds__(256) void ft_groups_kernel(const fnnue_pos* __restrict__ pos,
                                                         const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                        uint32_t base_index, int star, NetPtrs net,
+                                                        uint32_t lo, uint32_t hi, int star, NetPtrs net,
                                                         uint8_t* __restrict__ x, int32_t* __restrict__ psqt,
                                                         uint8_t* __restrict__ bucket_out,
                                                         uint32_t* __restrict__ err) {
@@ -245,14 +245,16 @@ __global__ __launch_bounds__(256) void ft_groups_kernel(const fnnue_pos* __restr
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   const u16 b_lo = u16::load(net.ft_bias, lane), b_hi = u16::load(net.ft_bias + HD / 2, lane);
   for (uint32_t g = wid; g < ngroups; g += nw) {
-    const uint32_t begin = off[g], end = off[g + 1];
+    // the group clamped to this launch's positions [lo, hi) (a group cut at lo
+    // restarts there with a refresh; malformed offsets give empty ranges)
+    const uint32_t begin = max(off[g], lo), end = min(off[g + 1], hi);
     // Base state (previous ply for CHAIN, parent for STAR).
     bool have = false;
     int base_pc = 0, base_wk = 0, base_bk = 0;
     u16 bw_lo = b_lo, bw_hi = b_hi, bb_lo = b_lo, bb_hi = b_hi;
     for (uint32_t i = begin; i < end; ++i) {
       const Decoded d = decode(pos + i, lane);
-      const uint32_t o = i - base_index;
+      const uint32_t o = i - lo;
       uint8_t* xo = x + (size_t)o * HD;
       if (!d.ok) {
         store_invalid<HD>(xo, lane);
@@ -530,13 +532,14 @@ hipError_t launch_scratch_t(const fnnue_pos* pos, uint32_t n, const NetPtrs& net
 }
 
 template <int HD>
-hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups, uint32_t base, int mode,
+hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups, uint32_t lo, uint32_t hi,
+                           int mode,
                            const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err,
                            hipStream_t stream) {
   uint32_t blocks = (ngroups + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   if (blocks == 0) return hipSuccess;
-  hipLaunchKernelGGL((ft_groups_kernel<HD, 4>), dim3(blocks), dim3(256), 0, stream, pos, off, ngroups, base,
+  hipLaunchKernelGGL((ft_groups_kernel<HD, 4>), dim3(blocks), dim3(256), 0, stream, pos, off, ngroups, lo, hi,
                      mode == FNNUE_GROUP_STAR, net, x, psqt, bucket, err);
   return hipGetLastError();
 }
@@ -583,10 +586,10 @@ hipError_t launch_ft_scratch(uint32_t hd, const fnnue_pos* pos, uint32_t n, cons
 #undef CALL
 }
 
-hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups, uint32_t base,
-                            int mode, const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err,
-                            hipStream_t stream) {
-#define CALL(H) launch_groups_t<H>(pos, off, ngroups, base, mode, net, x, psqt, bucket, err, stream)
+hipError_t launch_ft_groups(uint32_t hd, const fnnue_pos* pos, const uint32_t* off, uint32_t ngroups, uint32_t lo,
+                            uint32_t hi, int mode, const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket,
+                            uint32_t* err, hipStream_t stream) {
+#define CALL(H) launch_groups_t<H>(pos, off, ngroups, lo, hi, mode, net, x, psqt, bucket, err, stream)
   FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
 }

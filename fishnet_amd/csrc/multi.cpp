@@ -11,7 +11,8 @@
 //    count (fnnue_partition_groups);
 //  * host-buffer calls run one host thread per device (H2D of its shard, the
 //    device path, D2H into its disjoint slice of the caller's buffers);
-//    device-buffer calls enqueue on every device's stream and return.
+//    device-buffer calls enqueue on every device's stream (the caller's, or
+//    the context's own) and return without any host synchronisation.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -198,23 +199,31 @@ int fnnue_multi_eval_groups(fnnue_multi* m, const fnnue_pos* pos, size_t npos, c
   });
 }
 
+// Device-buffer calls: every device's work is enqueued on streams[i] (or, for
+// a null array / entry, its context's own stream) and the call returns; no
+// host synchronisation at any batch size, so the devices run concurrently.
+namespace {
+void* stream_of(void* const* streams, size_t i) { return streams ? streams[i] : nullptr; }
+}  // namespace
+
 int fnnue_multi_eval_positions_device(fnnue_multi* m, const fnnue_pos* const* d_pos, const size_t* n,
-                                      int32_t* const* d_psqt, int32_t* const* d_positional) {
+                                      int32_t* const* d_psqt, int32_t* const* d_positional, void* const* streams) {
   if (!m || !d_pos || !n || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null argument");
   for (size_t i = 0; i < m->ctx.size(); ++i)
-    if (int rc = fnnue_eval_positions_device(m->ctx[i], d_pos[i], n[i], d_psqt[i], d_positional[i], nullptr))
+    if (int rc = fnnue_eval_positions_device(m->ctx[i], d_pos[i], n[i], d_psqt[i], d_positional[i],
+                                             stream_of(streams, i)))
       return fail(rc, "device " + std::to_string(m->devices[i]) + ": " + fnnue_last_error());
   return FNNUE_OK;
 }
 
 int fnnue_multi_eval_groups_device(fnnue_multi* m, const fnnue_pos* const* d_pos, const uint32_t* const* d_off,
                                    const size_t* ngroups, const size_t* npos, int mode, int32_t* const* d_psqt,
-                                   int32_t* const* d_positional) {
+                                   int32_t* const* d_positional, void* const* streams) {
   if (!m || !d_pos || !d_off || !ngroups || !npos || !d_psqt || !d_positional)
     return fail(FNNUE_E_ARG, "null argument");
   for (size_t i = 0; i < m->ctx.size(); ++i)
     if (int rc = fnnue_eval_groups_device(m->ctx[i], d_pos[i], d_off[i], ngroups[i], npos[i], mode, d_psqt[i],
-                                          d_positional[i], nullptr))
+                                          d_positional[i], stream_of(streams, i)))
       return fail(rc, "device " + std::to_string(m->devices[i]) + ": " + fnnue_last_error());
   return FNNUE_OK;
 }
@@ -231,10 +240,11 @@ int fnnue_multi_eval_vpositions(fnnue_multi* m, const fnnue_vpos* pos, size_t n,
 }
 
 int fnnue_multi_eval_vpositions_device(fnnue_multi* m, const fnnue_vpos* const* d_pos, const size_t* n,
-                                       int32_t* const* d_psqt, int32_t* const* d_positional) {
+                                       int32_t* const* d_psqt, int32_t* const* d_positional, void* const* streams) {
   if (!m || !d_pos || !n || !d_psqt || !d_positional) return fail(FNNUE_E_ARG, "null argument");
   for (size_t i = 0; i < m->ctx.size(); ++i)
-    if (int rc = fnnue_eval_vpositions_device(m->ctx[i], d_pos[i], n[i], d_psqt[i], d_positional[i], nullptr))
+    if (int rc = fnnue_eval_vpositions_device(m->ctx[i], d_pos[i], n[i], d_psqt[i], d_positional[i],
+                                              stream_of(streams, i)))
       return fail(rc, "device " + std::to_string(m->devices[i]) + ": " + fnnue_last_error());
   return FNNUE_OK;
 }

@@ -287,6 +287,10 @@ def _sizes(vals) -> C.Array:
     return (C.c_size_t * len(vals))(*vals)
 
 
+def _streams(vals):
+    return None if vals is None else _ptrs([v or 0 for v in vals])
+
+
 class MultiEvaluator:
     """Several GPUs from one process (fnnue_multi_*): the net is RCCL-broadcast
     from devices[0]; batches are sharded without a data-path collective.  The
@@ -335,18 +339,21 @@ class MultiEvaluator:
                                               N.ptr(psqt), N.ptr(positional)))
         return psqt, positional
 
-    # device-resident shards: one pointer / count per device (asynchronous; then sync())
-    def eval_positions_device(self, d_pos, n, d_psqt, d_positional) -> None:
+    # device-resident shards: one pointer / count per device (asynchronous; then
+    # sync()).  streams: one hipStream_t handle per device (e.g. torch's
+    # current stream of each device) or None for the contexts' own streams.
+    def eval_positions_device(self, d_pos, n, d_psqt, d_positional, streams=None) -> None:
         N.check(N.lib.fnnue_multi_eval_positions_device(self._h, _ptrs(d_pos), _sizes(n), _ptrs(d_psqt),
-                                                        _ptrs(d_positional)))
+                                                        _ptrs(d_positional), _streams(streams)))
 
-    def eval_vpositions_device(self, d_pos, n, d_psqt, d_positional) -> None:
+    def eval_vpositions_device(self, d_pos, n, d_psqt, d_positional, streams=None) -> None:
         N.check(N.lib.fnnue_multi_eval_vpositions_device(self._h, _ptrs(d_pos), _sizes(n), _ptrs(d_psqt),
-                                                         _ptrs(d_positional)))
+                                                         _ptrs(d_positional), _streams(streams)))
 
-    def eval_groups_device(self, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional) -> None:
+    def eval_groups_device(self, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional, streams=None) -> None:
         N.check(N.lib.fnnue_multi_eval_groups_device(self._h, _ptrs(d_pos), _ptrs(d_off), _sizes(ngroups),
-                                                     _sizes(npos), mode, _ptrs(d_psqt), _ptrs(d_positional)))
+                                                     _sizes(npos), mode, _ptrs(d_psqt), _ptrs(d_positional),
+                                                     _streams(streams)))
 
     def sync(self) -> None:
         N.check(N.lib.fnnue_multi_sync(self._h))

@@ -169,21 +169,24 @@ int fnnue_multi_eval_positions(fnnue_multi *m, const fnnue_pos *pos, size_t n, i
 int fnnue_multi_eval_groups(fnnue_multi *m, const fnnue_pos *pos, size_t npos, const uint32_t *off, size_t ngroups,
                             int mode, int32_t *psqt, int32_t *positional);
 /* Device buffers: arrays of one pointer / count per device (device i's
- * buffers live on device i); enqueued on each context's own stream, returns
- * without synchronising.  fnnue_multi_sync drains every device and reports
- * latched errors (as fnnue_ctx_check). */
+ * buffers live on device i); device i's work is enqueued on streams[i] (a
+ * hipStream_t of device i, as void*) or, when `streams` or streams[i] is NULL,
+ * on its context's own stream, so the caller can order it after the work that
+ * wrote the inputs (or synchronise first).  Returns without synchronising the
+ * host, at any batch size.  fnnue_multi_sync waits for every device's
+ * context work and reports latched errors (as fnnue_ctx_check). */
 int fnnue_multi_eval_positions_device(fnnue_multi *m, const fnnue_pos *const *d_pos, const size_t *n,
-                                      int32_t *const *d_psqt, int32_t *const *d_positional);
+                                      int32_t *const *d_psqt, int32_t *const *d_positional, void *const *streams);
 int fnnue_multi_eval_groups_device(fnnue_multi *m, const fnnue_pos *const *d_pos, const uint32_t *const *d_off,
                                    const size_t *ngroups, const size_t *npos, int mode, int32_t *const *d_psqt,
-                                   int32_t *const *d_positional);
+                                   int32_t *const *d_positional, void *const *streams);
 int fnnue_multi_sync(fnnue_multi *m);
 /* Fairy-Stockfish variant positions over every device of a multi built from a
  * variant net (BASELINE config 5 on 8 GPUs): contiguous shards, as
  * fnnue_multi_eval_positions[_device]. */
 int fnnue_multi_eval_vpositions(fnnue_multi *m, const fnnue_vpos *pos, size_t n, int32_t *psqt, int32_t *positional);
 int fnnue_multi_eval_vpositions_device(fnnue_multi *m, const fnnue_vpos *const *d_pos, const size_t *n,
-                                       int32_t *const *d_psqt, int32_t *const *d_positional);
+                                       int32_t *const *d_psqt, int32_t *const *d_positional, void *const *streams);
 /* Splits groups off[0..ngroups] into nparts contiguous runs of whole groups
  * with about equal position counts: part k = groups [cut[k], cut[k+1]),
  * cut has nparts + 1 entries.  Host only. */

@@ -109,8 +109,9 @@ def test_chunk_boundary_wide_net(ev_cache):
     gpos, off = F.random_playouts(32, 9000, mode=N.PLAYOUT_PLIES, threads=8)
     assert off[-1] > chunk
     gs, go = ev.eval_groups(gpos, off, N.GROUP_CHAIN)
-    cut = int(np.searchsorted(off, chunk, side="right")) - 1  # first group of the second chunk
-    idx = np.r_[0:2000, int(off[cut]) - 2000:int(off[cut]) + 2000, len(gpos) - 2000:len(gpos)]
+    # chunks are cut at fixed positions: the game straddling position `chunk`
+    # restarts with a refresh there
+    idx = np.r_[0:2000, chunk - 2000:chunk + 2000, len(gpos) - 2000:len(gpos)]
     ops, opo, rc = on.eval_packed(gpos[idx], threads=8)
     assert np.array_equal(gs[idx], ops) and np.array_equal(go[idx], opo)
 
@@ -320,7 +321,7 @@ def test_groups_device_latched_invalid(ev_cache):
 
 
 def test_device_groups_offsets_checked_on_device(ev_cache):
-    """fnnue_eval_groups_device never reads the offsets on the host (one launch):
+    """fnnue_eval_groups_device never reads the offsets on the host (any size):
     malformed offsets latch FNNUE_E_ARG, stay in bounds, and the ctx stays usable;
     arbitrary (valid) groupings give the oracle's results."""
     import torch
@@ -410,6 +411,77 @@ def test_device_calls_on_two_streams(ev_cache):
         idx = np.arange(0, len(pos), 13)
         ops, opo, rc = on.eval_packed(pos[idx], threads=8)
         assert np.array_equal(ps.cpu().numpy()[idx], ops) and np.array_equal(po.cpu().numpy()[idx], opo)
+
+
+def test_device_call_after_its_stream_was_destroyed(ev_cache):
+    """A *_device call on a temporary stream, the stream destroyed right after,
+    then calls on the context's own stream and on another stream: the library
+    never touches the destroyed stream again (the workspace event is recorded
+    on each call's own stream), results exact."""
+    import torch
+    ev, on = ev_cache()
+    pos = F.random_playouts(43, 50_000, threads=8)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(pos).to(dev)
+    outs = [torch.zeros(len(pos), dtype=torch.int32, device=dev) for _ in range(6)]
+    torch.cuda.synchronize()
+    tmp = torch.cuda.Stream(dev)
+    ev.eval_positions_device(d.data_ptr(), len(pos), outs[0].data_ptr(), outs[1].data_ptr(), tmp.cuda_stream)
+    tmp.synchronize()
+    del tmp  # torch destroys the stream (or returns it to its pool)
+    ev.eval_positions_device(d.data_ptr(), len(pos), outs[2].data_ptr(), outs[3].data_ptr(), None)
+    ev.check()
+    s2 = torch.cuda.Stream(dev)
+    ev.eval_positions_device(d.data_ptr(), len(pos), outs[4].data_ptr(), outs[5].data_ptr(), s2.cuda_stream)
+    ev.check()  # waits for the last call's stream too, without draining the device
+    idx = np.arange(0, len(pos), 7)
+    ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+    assert rc == 0
+    for k in (0, 2, 4):
+        assert np.array_equal(outs[k].cpu().numpy()[idx], ops) and np.array_equal(outs[k + 1].cpu().numpy()[idx], opo)
+
+
+def test_device_groups_above_one_workspace(ev_cache):
+    """A grouped *_device call above one workspace (> 2^20 positions): cut into
+    chunks at fixed positions on the device, the offsets never read on the
+    host.  STAR (every ply + children of 560 games, ~1.4M) and CHAIN (every
+    ply of 20k games, ~1.6M) against the oracle, for both FT
+    implementations; groups cut by a chunk boundary included; malformed
+    offsets still latch FNNUE_E_ARG at this size."""
+    import torch
+    ev, on = ev_cache()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    for mode, pm, count, seed in ((N.GROUP_STAR, N.PLAYOUT_CHILDREN, 560, 51), (N.GROUP_CHAIN, N.PLAYOUT_PLIES, 20_000, 52)):
+        pos, off = F.random_playouts(seed, count, mode=pm, threads=8)
+        n = len(pos)
+        assert n > (1 << 20)
+        # a group straddles the first chunk boundary
+        g = int(np.searchsorted(off, 1 << 20, side="right")) - 1
+        assert off[g] < (1 << 20) < off[g + 1]
+        d = torch.from_numpy(pos).to(dev)
+        d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert rc == 0
+        for impl in (N.FT_SLICED, N.FT_GATHER):
+            ev.set_ft_impl(impl)
+            try:
+                ps = torch.full((n,), 7, dtype=torch.int32, device=dev)
+                po = torch.full((n,), 7, dtype=torch.int32, device=dev)
+                ev.eval_groups_device(d.data_ptr(), d_off.data_ptr(), len(off) - 1, n, mode, ps.data_ptr(),
+                                      po.data_ptr(), stream)
+                ev.check()
+                assert np.array_equal(ps.cpu().numpy(), ops) and np.array_equal(po.cpu().numpy(), opo), (mode, impl)
+                bad = off.copy()
+                bad[len(bad) // 2] = bad[len(bad) // 2 + 1] + 1  # not non-decreasing, past the first chunk
+                d_bad = torch.from_numpy(bad.view(np.int32)).to(dev)
+                ev.eval_groups_device(d.data_ptr(), d_bad.data_ptr(), len(bad) - 1, n, mode, ps.data_ptr(),
+                                      po.data_ptr(), stream)
+                with pytest.raises(F.FnnueError) as e:
+                    ev.check()
+                assert e.value.name == "FNNUE_E_ARG"
+            finally:
+                ev.set_ft_impl(N.FT_SLICED)
 
 
 @pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (6, 2048, 0), (8, 1536, N.SYNTH_LEB128)])

@@ -12,8 +12,18 @@
   path with the big (HD 1024) and the small (HD 128) net, every ply of both
   compared with the oracle.
 
+The multi-GPU entry points at full per-GPU size (ndev = 1 here; the 2/8-GPU
+runs use exactly these calls with more devices):
+* test_config4_shard_multi_groups_device — a config-4 shard (>= 12.5M
+  positions = 1e8 / 8 GPUs, STAR) through fnnue_multi_eval_groups_device:
+  above one workspace, so the device cuts it into chunks with no host sync.
+* test_config3_multi_groups — config 3 (10k games, CHAIN) through
+  fnnue_multi_eval_groups with the HD 1024 and HD 128 nets.
+* test_config5_multi_vpositions_device — 1M crazyhouse and 1M atomic
+  positions through fnnue_multi_eval_vpositions_device.
+
 FNNUE_FULL=<positions> overrides the config-4 size (default 1e8).  JSON
-records go to gpurun_out/full_parity.json and gpurun_out/config3_full.json.
+records go to gpurun_out/<name>.json (one line each also on stdout).
 Host cost on the GPU box (16 threads): ~10 s generation, ~20 s oracle.
 """
 import json
@@ -150,4 +160,128 @@ def test_config3_full_size():
         rec["nets"][f"hd{hd}"] = {"mismatches_vs_oracle": m, "gpu_host_api_s": round(t_gpu, 3)}
     _record("config3_full.json", rec)
     assert n > 700_000
+    assert bad == 0
+
+
+def _multi_groups_device(m, pos, off, mode):
+    import torch
+    dev = torch.device("cuda", 0)
+    n = len(pos)
+    d_pos = torch.from_numpy(pos).to(dev)
+    d_off = torch.from_numpy(off.astype(np.uint32).view(np.int32)).to(dev)
+    d_ps = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    d_po = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    cur = [torch.cuda.current_stream(dev).cuda_stream]
+    t = time.perf_counter()
+    m.eval_groups_device([d_pos.data_ptr()], [d_off.data_ptr()], [len(off) - 1], [n], mode, [d_ps.data_ptr()],
+                         [d_po.data_ptr()], cur)
+    t_enq = time.perf_counter() - t
+    m.sync()
+    t_all = time.perf_counter() - t
+    return d_ps.cpu().numpy(), d_po.cpu().numpy(), t_enq, t_all
+
+
+@pytest.mark.timeout(600)
+def test_config4_shard_multi_groups_device():
+    """BASELINE config 4 per GPU: 1e8 / 8 = 12.5M positions (random games of
+    seed 3 + all legal 1-ply children, STAR) through
+    fnnue_multi_eval_groups_device at ndev = 1; every result vs the oracle."""
+    threads = _threads()
+    want = int(os.environ.get("FNNUE_CONFIG4_SHARD", "12500000"))
+    parts, offs, base, seed, total = [], [np.zeros(1, np.int64)], 0, 3, 0
+    while total < want:
+        p, o = F.random_playouts(seed, 2000, 0, 160, mode=F.PLAYOUT_CHILDREN, threads=threads)
+        parts.append(p)
+        offs.append(o[1:].astype(np.int64) + base)
+        base += len(p)
+        total += len(p)
+        seed += 7919
+    pos, off = np.concatenate(parts), np.concatenate(offs)
+    del parts
+    n = len(pos)
+    data = net_bytes(1, 1024, 0)
+    m = F.MultiEvaluator(F.Net.from_bytes(data), [0])
+    try:
+        ps, po, t_enq, t_all = _multi_groups_device(m, pos, off, F.GROUP_STAR)
+    finally:
+        m.close()
+    on = OracleNet(data)
+    mism = 0
+    for lo in range(0, n, 5_000_000):
+        hi = min(n, lo + 5_000_000)
+        ops, opo, rc = on.eval_packed(pos[lo:hi], threads=threads)
+        assert rc == 0
+        mism += int(((ops != ps[lo:hi]) | (opo != po[lo:hi])).sum())
+    _record("config4_shard_multi.json", {
+        "test": "tests/test_gpu_full.py::test_config4_shard_multi_groups_device",
+        "baseline_config": "config 4: 100M 1-ply children positions over 8 GPUs -> one GPU's shard",
+        "entry_point": "fnnue_multi_eval_groups_device (ndev = 1, STAR)",
+        "positions": n, "groups": len(off) - 1, "chunks": -(-n // (1 << 20)),
+        "enqueue_ms": round(t_enq * 1e3, 3), "call_to_sync_s": round(t_all, 3),
+        "mismatches_vs_oracle": mism})
+    assert n >= want
+    assert mism == 0
+
+
+@pytest.mark.timeout(600)
+def test_config3_multi_groups():
+    """BASELINE config 3: 10k games (seed 2), every ply, CHAIN, big HD 1024 +
+    small HD 128 net, through fnnue_multi_eval_groups (host buffers)."""
+    threads = _threads()
+    pos, off = F.random_playouts(2, 10_000, 0, 160, mode=F.PLAYOUT_PLIES, threads=threads)
+    rec = {"test": "tests/test_gpu_full.py::test_config3_multi_groups",
+           "baseline_config": "config 3: 10k-game corpus, incremental along move sequences, big + small net",
+           "entry_point": "fnnue_multi_eval_groups (ndev = 1, CHAIN)", "positions": len(pos),
+           "games": len(off) - 1, "nets": {}}
+    bad = 0
+    for hd, seed in ((1024, 1), (128, 1001)):
+        data = net_bytes(seed, hd, 0)
+        m = F.MultiEvaluator(F.Net.from_bytes(data), [0])
+        try:
+            ps, po = m.eval_groups(pos, off, F.GROUP_CHAIN)
+        finally:
+            m.close()
+        ops, opo, rc = OracleNet(data).eval_packed(pos, threads=threads)
+        assert rc == 0
+        k = int(((ps != ops) | (po != opo)).sum())
+        bad += k
+        rec["nets"][f"hd{hd}"] = {"mismatches_vs_oracle": k}
+    _record("config3_multi.json", rec)
+    assert len(pos) > 700_000
+    assert bad == 0
+
+
+@pytest.mark.timeout(600)
+def test_config5_multi_vpositions_device():
+    """BASELINE config 5: 1M crazyhouse and 1M atomic random-walk positions
+    through fnnue_multi_eval_vpositions_device (HD 1024 synthetic variant
+    nets), every result vs the variant oracle (parity unpinned: DESIGN §3)."""
+    import torch
+    from oracle.oracle import VariantOracleNet
+    threads = _threads()
+    dev = torch.device("cuda", 0)
+    rec = {"test": "tests/test_gpu_full.py::test_config5_multi_vpositions_device",
+           "baseline_config": "config 5: Fairy-Stockfish variant NNUE (crazyhouse / atomic) batched eval",
+           "entry_point": "fnnue_multi_eval_vpositions_device (ndev = 1)", "variants": {}}
+    bad = 0
+    for name, variant, seed in (("crazyhouse", F.VARIANT_CRAZYHOUSE, 5), ("atomic", F.VARIANT_ATOMIC, 6)):
+        data = F.synthesize_variant_net(seed, 1024, variant)
+        pos = F.random_vpositions(seed, variant, 1_000_000, 160)
+        m = F.MultiEvaluator(F.Net.from_bytes_variant(data, variant), [0])
+        try:
+            d_pos = torch.from_numpy(pos).to(dev)
+            d_ps = torch.full((len(pos),), -1, dtype=torch.int32, device=dev)
+            d_po = torch.full((len(pos),), -1, dtype=torch.int32, device=dev)
+            m.eval_vpositions_device([d_pos.data_ptr()], [len(pos)], [d_ps.data_ptr()], [d_po.data_ptr()],
+                                     [torch.cuda.current_stream(dev).cuda_stream])
+            m.sync()
+            ps, po = d_ps.cpu().numpy(), d_po.cpu().numpy()
+        finally:
+            m.close()
+        ops, opo, rc = VariantOracleNet(data, variant).eval_packed(pos, threads=threads)
+        assert rc == 0
+        k = int(((ps != ops) | (po != opo)).sum())
+        bad += k
+        rec["variants"][name] = {"positions": len(pos), "mismatches_vs_oracle": k}
+    _record("config5_multi.json", rec)
     assert bad == 0

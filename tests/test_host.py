@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert N.lib.fnnue_abi_version() >> 16 == 2  # 2.0: fnnue_eval_groups takes npos
+    assert N.lib.fnnue_abi_version() >> 16 == 3  # 3.0: the fnnue_multi_*_device calls take streams
 
 
 def test_net_parse_and_info():

@@ -137,7 +137,8 @@ def test_multi_single_device_matches_oracle():
         d_pos = torch.from_numpy(pos).to(dev)
         d_ps = torch.zeros(len(pos), dtype=torch.int32, device=dev)
         d_po = torch.zeros(len(pos), dtype=torch.int32, device=dev)
-        m.eval_positions_device([d_pos.data_ptr()], [len(pos)], [d_ps.data_ptr()], [d_po.data_ptr()])
+        cur = [torch.cuda.current_stream(dev).cuda_stream]  # ordered after the zero fills above
+        m.eval_positions_device([d_pos.data_ptr()], [len(pos)], [d_ps.data_ptr()], [d_po.data_ptr()], cur)
         m.sync()
         assert np.array_equal(d_ps.cpu().numpy(), ps) and np.array_equal(d_po.cpu().numpy(), po)
         d_off = torch.from_numpy(off.view(np.int32)).to(dev)
@@ -145,7 +146,7 @@ def test_multi_single_device_matches_oracle():
         d_gs = torch.zeros(len(gpos), dtype=torch.int32, device=dev)
         d_go = torch.zeros(len(gpos), dtype=torch.int32, device=dev)
         m.eval_groups_device([d_g.data_ptr()], [d_off.data_ptr()], [len(off) - 1], [len(gpos)], F.GROUP_STAR,
-                             [d_gs.data_ptr()], [d_go.data_ptr()])
+                             [d_gs.data_ptr()], [d_go.data_ptr()], cur)
         m.sync()
         assert np.array_equal(d_gs.cpu().numpy(), gs) and np.array_equal(d_go.cpu().numpy(), go)
         assert m.ctx(0).device == 0
