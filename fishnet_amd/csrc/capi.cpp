@@ -221,10 +221,6 @@ int finish_upload(fnnue_ctx* c) {
     const char* env = std::getenv("FNNUE_SWAR");
     c->plan.swar = c->acc_bound < 32768 && !(env && env[0] == '0');
   }
-  if (std::getenv("FNNUE_DEBUG_SKIP_RELAYOUT")) {  // diagnostics only: gather path without tiles
-    c->ft_impl = FNNUE_FT_GATHER;
-    return FNNUE_OK;
-  }
   if (c->variant == kVariantChess)
     HIP_TRY(launch_relayout_sliced(c->hd, c->ptrs, c->plan.tiles, c->stream), "relayout launch");
   else
@@ -681,29 +677,6 @@ int fnnue_eval_vpositions_device(fnnue_ctx* ctx, const fnnue_vpos* d_pos, size_t
       return rc;
   }
   return FNNUE_OK;
-}
-
-// Diagnostics (not in fnnue.h): runs the variant plan on n <= chunk host
-// positions and copies the plan back: ctr words, units (int4), items, lists.
-int fnnue_debug_variant_plan(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t n, uint32_t* ctr, size_t ctr_words,
-                             int32_t* units, size_t units_cap, uint32_t* items, uint16_t* flist, uint32_t* perm,
-                             uint8_t* bucket) {
-  if (!ctx || ctx->variant == kVariantChess || n == 0 || n > ctx->chunk) return fail(FNNUE_E_ARG, "bad argument");
-  DeviceGuard g(ctx->device);
-  int rc = ensure_stage(ctx, n, 0);
-  if (rc) return rc;
-  fnnue_vpos* d = reinterpret_cast<fnnue_vpos*>(ctx->d_pos);
-  HIP_TRY(hipMemcpy(d, pos, n * sizeof(fnnue_vpos), hipMemcpyHostToDevice), "H2D");
-  HIP_TRY(launch_variant_plan(d, (uint32_t)n, ctx->variant, ctx->plan, ctx->d_psqt, ctx->bucket, ctx->err, ctx->stream),
-          "plan");
-  HIP_TRY(hipStreamSynchronize(ctx->stream), "sync");
-  HIP_TRY(hipMemcpy(ctr, ctx->plan.ctr, std::min(ctr_words, variant_ctr_words()) * 4, hipMemcpyDeviceToHost), "D2H");
-  HIP_TRY(hipMemcpy(units, ctx->plan.units, units_cap * 16, hipMemcpyDeviceToHost), "D2H");
-  HIP_TRY(hipMemcpy(items, ctx->plan.items, 2 * n * 4, hipMemcpyDeviceToHost), "D2H");
-  HIP_TRY(hipMemcpy(flist, ctx->plan.flist, 2 * n * 64, hipMemcpyDeviceToHost), "D2H");
-  HIP_TRY(hipMemcpy(perm, ctx->plan.perm, n * 4, hipMemcpyDeviceToHost), "D2H");
-  HIP_TRY(hipMemcpy(bucket, ctx->bucket, n, hipMemcpyDeviceToHost), "D2H");
-  return latched(ctx);
 }
 
 int fnnue_eval_vpositions(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t n, int32_t* psqt, int32_t* positional) {

@@ -90,11 +90,7 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
   }
   __syncthreads();
   for (int i = threadIdx.x; i < kBins; i += blockDim.x)
-#ifdef FT_EXP_NO_ATOMIC
-    lbase[i] = lcnt[i] ? ctr[kOff + i] + (blockIdx.x * 7u) % 64u : 0;
-#else
     lbase[i] = lcnt[i] ? atomicAdd(&ctr[kCur + i], lcnt[i]) : 0;
-#endif
   __syncthreads();
   if (!live) return;
   const uint32_t slot = lbase[kp] + rp;
@@ -107,10 +103,8 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
   const int bucket = (b.cnt - 1) >> 2;
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
   uint32_t* mine = lists + threadIdx.x * kListStrideWords;
-#ifndef PLAN_EXP_NO_ROWS
   write_rows(b, 0, b.wk, iw, ctr, mine, flist);
   write_rows(b, 1, b.bk, ib, ctr, mine, flist);
-#endif
   items[iw] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;
@@ -150,11 +144,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
   // item's half of row `slot` of x.
   const uint32_t xoff = (rec & kItemRowMask) * (HD / 2) + 32 * s + 4 * q;
   const uint32_t xv = kSwar ? transform4_swar(lo, hi) : transform4(lo, hi);
-#ifdef FT_EXP_NO_STORE
-  if (xv == 0x12345678u)
-#endif
   __builtin_amdgcn_raw_buffer_store_b32(xv, x_rsrc, xoff, 0, 0);
-#ifndef FT_EXP_NO_PSQT
   if constexpr (kPsqt) {
     // PSQT part of this perspective: sum of psqtWeights[row][bucket] (int32
     // wrap), own king included, in the fetch layout: lane l holds entries
@@ -175,7 +165,6 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
     __builtin_amdgcn_raw_buffer_store_b32((int32_t)a2, psqt_rsrc,
                                           (lane & 7) == 0 ? (reci & kItemRowMask) * 4u : kDroppedOffset, 0, 0);
   }
-#endif
 }
 
 // One workgroup = one (unit, slice).  16 waves x 8 items per pass; records and
@@ -218,11 +207,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   uint4 t[kTileLoads];
 #pragma unroll
   for (int k = 0; k < kTileLoads; ++k)
-#ifdef FT_EXP_NO_TILE
-    t[k] = make_uint4(k, 0, 0, 0);
-#else
     t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
-#endif
   uint4 pt[2];
   const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * G::kRows * kPsqtBuckets);
   if (s == 0) {
@@ -278,16 +263,12 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
     constexpr bool kPsqt = decltype(psqt)::value;
     while (base < u.z) {
       const PassFetch cur = fa;
-#ifndef FT_EXP_REUSE_LIST
       fa = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
-#endif
       slice_pass<HD, kSwar, kPsqt>(cur, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc, x_rsrc);
       base += 128;
       if (base >= u.z) break;
       const PassFetch cur2 = fb;
-#ifndef FT_EXP_REUSE_LIST
       fb = fetch_pass(items_rsrc, flist_rsrc, base + 256, last, lane, it_in_wave);
-#endif
       slice_pass<HD, kSwar, kPsqt>(cur2, lb, lane, it_in_wave, s, q, lbase, b_lo, b_hi, krow, ptile, psqt_rsrc,
                                    x_rsrc);
       base += 128;

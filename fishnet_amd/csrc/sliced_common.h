@@ -413,12 +413,8 @@ __device__ __forceinline__ PassFetch fetch_pass(__amdgpu_buffer_rsrc_t items, __
   PassFetch f;
   f.rec = __builtin_amdgcn_raw_buffer_load_b32(items, (uint32_t)min(pass_base + it_in_wave, last) * 4u, 0, 0);
   const uint32_t li = (uint32_t)min(pass_base + (lane >> 3), last);
-#ifdef FT_EXP_NO_LIST
-  f.lst = make_uint2(f.rec & 0x70, f.rec & 0x30);
-#else
   const u32x2 l = __builtin_amdgcn_raw_buffer_load_b64(flist, li * 64u + 8u * (uint32_t)(lane & 7), 0, 0);
   f.lst = make_uint2(l.x, l.y);
-#endif
   return f;
 }
 

@@ -1,6 +1,9 @@
 #!/bin/bash
 # Builds an experimental variant of libfnnue.so with extra -D flags on every
-# HIP source into exp/libfnnue_<name>.so (run bench with FNNUE_LIB=...).
+# HIP source (the tunables FT_UNIT_ITEMS, SEG_UNIT_PLIES, PLAN_WG, FT_DEPTH;
+# knock-out experiments are patched into a scratch copy, never the shipped
+# sources)
+# into exp/libfnnue_<name>.so (run bench with FNNUE_LIB=...).
 #   usage: tools/exp_build.sh <name> [-DFLAG ...]
 set -euo pipefail
 cd "$(dirname "$0")/../fishnet_amd/csrc"
