@@ -63,6 +63,7 @@ SIGNATURES = {
     "fnnue_net_load_mem": ([_vp, _sz, _P(_vp)], _i32),
     "fnnue_net_info": ([_vp, _P(_u32), _P(_u32), _P(C.c_char_p)], _i32),
     "fnnue_net_free": ([_vp], None),
+    "fnnue_net_sha256": ([_vp, _vp], _i32),
     "fnnue_net_synthesize": ([_u64, _u32, _u32, _P(_vp), _P(_sz)], _i32),
     "fnnue_buffer_free": ([_vp], None),
     "fnnue_device_count": ([_P(_i32)], _i32),

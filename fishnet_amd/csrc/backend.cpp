@@ -156,17 +156,23 @@ int fnnue_backend::analysis(Job& j, const std::vector<size_t>& games_in, std::ve
     HIP_TRY(hipMemcpyAsync(text.p, t.data(), t.size(), hipMemcpyHostToDevice, s), "H2D(text)");
     HIP_TRY(hipMemcpyAsync(fen_off.p, fo.data(), fo.size() * 4, hipMemcpyHostToDevice, s), "H2D(fen offsets)");
     HIP_TRY(hipMemcpyAsync(mv_off.p, mo.data(), mo.size() * 4, hipMemcpyHostToDevice, s), "H2D(move offsets)");
+    // The builder names the failing game; that batch fails (PositionFailed)
+    // and the rest are retried.  A game index outside the batch cannot be
+    // blamed on any batch: the whole call fails instead.
     auto drop = [&](const BuildResult& R) {
-      const size_t g = R.err_game < ng ? R.err_game : 0;
-      j.rc[live[g]] = R.err_code == kBuildErrFen ? FNNUE_E_FEN : FNNUE_E_MOVE;
-      live.erase(live.begin() + (long)g);
+      if (R.err_game >= ng)
+        return fail(FNNUE_E_DEVICE, "batch builder reported game " + std::to_string(R.err_game) + " of " +
+                                        std::to_string(ng));
+      j.rc[live[R.err_game]] = R.err_code == kBuildErrFen ? FNNUE_E_FEN : FNNUE_E_MOVE;
+      live.erase(live.begin() + (long)R.err_game);
+      return (int)FNNUE_OK;
     };
     // sizing pass, then the outputs (both synchronise the stream)
     BuildResult R = build_batch_device(text.as<char>(), fen_off.as<uint32_t>(), mv_off.as<uint32_t>(), ng, false,
                                        nullptr, 0, nullptr, 0, s);
     if (R.hip != hipSuccess) return hip_fail(R.hip, "device batch builder");
     if (R.err_code) {
-      drop(R);
+      if (int rc = drop(R)) return rc;
       continue;
     }
     const size_t n = R.n_out;
@@ -178,7 +184,7 @@ int fnnue_backend::analysis(Job& j, const std::vector<size_t>& games_in, std::ve
                            pos.as<fnnue_pos>(), n, goff.as<uint32_t>(), ng + 1, s);
     if (R.hip != hipSuccess) return hip_fail(R.hip, "device batch builder");
     if (R.err_code) {
-      drop(R);
+      if (int rc = drop(R)) return rc;
       continue;
     }
     if (R.capacity || R.n_out != n || R.n_groups != ng) return fail(FNNUE_E_DEVICE, "batch builder sizes changed");

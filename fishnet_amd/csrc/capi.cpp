@@ -22,6 +22,7 @@
 #include "internal.h"
 #include "kernels.h"
 #include "net.h"
+#include "sha256.h"
 
 using namespace fnnue;
 using namespace fnnue::detail;
@@ -325,6 +326,7 @@ int fnnue_net_load_mem(const void* buf, size_t len, fnnue_net** out) {
   } catch (const std::bad_alloc&) {
     return fail(FNNUE_E_OOM, "host allocation failed");
   }
+  sha256(static_cast<const uint8_t*>(buf), len, n->sha256);
   *out = n.release();
   return FNNUE_OK;
 }
@@ -343,20 +345,51 @@ int fnnue_net_load_variant_mem(const void* buf, size_t len, int variant, fnnue_n
   } catch (const std::bad_alloc&) {
     return fail(FNNUE_E_OOM, "host allocation failed");
   }
+  sha256(static_cast<const uint8_t*>(buf), len, n->sha256);
   *out = n.release();
   return FNNUE_OK;
 }
 
-int fnnue_net_load_variant(const char* path, int variant, fnnue_net** out) {
-  if (!path || !out) return fail(FNNUE_E_ARG, "null argument");
-  *out = nullptr;
+namespace {
+
+int read_file(const char* path, std::vector<uint8_t>& buf) {
   std::ifstream f(path, std::ios::binary | std::ios::ate);
   if (!f) return fail(FNNUE_E_IO, std::string("cannot open ") + path);
   const std::streamsize len = f.tellg();
   f.seekg(0);
-  std::vector<uint8_t> buf((size_t)len);
+  try {
+    buf.resize((size_t)len);
+  } catch (const std::bad_alloc&) {
+    return fail(FNNUE_E_OOM, "host allocation failed");
+  }
   if (!f.read(reinterpret_cast<char*>(buf.data()), len)) return fail(FNNUE_E_IO, std::string("cannot read ") + path);
-  return fnnue_net_load_variant_mem(buf.data(), buf.size(), variant, out);
+  return FNNUE_OK;
+}
+
+// Net identity: a file named nn-<12 hex>.nnue claims that its SHA-256 starts
+// with those digits (upstream's net naming; [ref] build.rs:7 pins
+// nn-ad9b42354671.nnue and build.rs:100-112 deletes a corrupt download).
+// A mismatch is a corrupt or renamed file: FNNUE_E_FORMAT, the net freed.
+int check_identity(const char* path, fnnue_net** out) {
+  const std::string claim = net_name_digest_prefix(path);
+  if (claim.empty()) return FNNUE_OK;
+  const std::string got = hex_lower((*out)->sha256, 32);
+  if (got.compare(0, 12, claim) == 0) return FNNUE_OK;
+  fnnue_net_free(*out);
+  *out = nullptr;
+  return fail(FNNUE_E_FORMAT, std::string(path) + ": SHA-256 " + got.substr(0, 12) + "... does not match the name's " +
+                                  claim + " (corrupt or renamed net file)");
+}
+
+}  // namespace
+
+int fnnue_net_load_variant(const char* path, int variant, fnnue_net** out) {
+  if (!path || !out) return fail(FNNUE_E_ARG, "null argument");
+  *out = nullptr;
+  std::vector<uint8_t> buf;
+  if (int rc = read_file(path, buf)) return rc;
+  if (int rc = fnnue_net_load_variant_mem(buf.data(), buf.size(), variant, out)) return rc;
+  return check_identity(path, out);
 }
 
 int fnnue_net_variant(const fnnue_net* net, int* variant) {
@@ -368,13 +401,16 @@ int fnnue_net_variant(const fnnue_net* net, int* variant) {
 int fnnue_net_load(const char* path, fnnue_net** out) {
   if (!path || !out) return fail(FNNUE_E_ARG, "null argument");
   *out = nullptr;
-  std::ifstream f(path, std::ios::binary | std::ios::ate);
-  if (!f) return fail(FNNUE_E_IO, std::string("cannot open ") + path);
-  const std::streamsize len = f.tellg();
-  f.seekg(0);
-  std::vector<uint8_t> buf((size_t)len);
-  if (!f.read(reinterpret_cast<char*>(buf.data()), len)) return fail(FNNUE_E_IO, std::string("cannot read ") + path);
-  return fnnue_net_load_mem(buf.data(), buf.size(), out);
+  std::vector<uint8_t> buf;
+  if (int rc = read_file(path, buf)) return rc;
+  if (int rc = fnnue_net_load_mem(buf.data(), buf.size(), out)) return rc;
+  return check_identity(path, out);
+}
+
+int fnnue_net_sha256(const fnnue_net* net, uint8_t* digest) {
+  if (!net || !digest) return fail(FNNUE_E_ARG, "null argument");
+  std::memcpy(digest, net->sha256, 32);
+  return FNNUE_OK;
 }
 
 int fnnue_net_info(const fnnue_net* net, uint32_t* hd, uint32_t* file_hash, const char** desc) {
@@ -870,7 +906,7 @@ int fnnue_random_playouts(uint64_t seed, size_t count, uint32_t min_plies, uint3
     Part& P = parts[t];
     for (size_t i = b; i < e; ++i) {
       uint64_t st = seed ^ (0xD1B54A32D192ED03ull * (i + 1));
-      const uint32_t L = min_plies + (uint32_t)(splitmix64(st) % (uint64_t)(max_plies - min_plies + 1));
+      const uint32_t L = min_plies + (uint32_t)(splitmix64(st) % ((uint64_t)max_plies - min_plies + 1));
       Board bd = start;
       auto emit = [&](const Board& x) {
         if (mode == FNNUE_PLAYOUT_PLIES) {

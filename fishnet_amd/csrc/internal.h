@@ -14,6 +14,7 @@
 
 struct fnnue_net {
   fnnue::Net net;
+  uint8_t sha256[32] = {};  // SHA-256 of the file bytes (net identity, fnnue_net_sha256)
 };
 
 struct fnnue_ctx {

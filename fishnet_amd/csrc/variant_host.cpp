@@ -196,7 +196,7 @@ int fnnue_random_vpositions(uint64_t seed, int variant, size_t count, uint32_t m
   try {
     for (size_t i = 0; i < count; ++i) {
       uint64_t st = seed ^ (0xD1B54A32D192ED03ull * (i + 1));
-      const uint32_t L = (uint32_t)(splitmix64(st) % (uint64_t)(max_plies + 1));
+      const uint32_t L = (uint32_t)(splitmix64(st) % ((uint64_t)max_plies + 1));
       VState v;
       start_position(v);
       if (mode == FNNUE_PLAYOUT_PLIES) res.push_back(pack_v(v));

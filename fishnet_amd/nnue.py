@@ -73,6 +73,12 @@ class Net:
         N.check(N.lib.fnnue_net_info(self._h, C.byref(hd), C.byref(fh), C.byref(desc)))
         return hd.value, fh.value, desc.value.decode(errors="replace")
 
+    def sha256(self) -> str:
+        """SHA-256 of the file bytes, lowercase hex (net identity)."""
+        d = (C.c_uint8 * 32)()
+        N.check(N.lib.fnnue_net_sha256(self._h, d))
+        return bytes(d).hex()
+
     def accumulator_bound(self) -> int:
         """Largest possible |sum| of an even accumulator column (< 2^15: SWAR rows exact)."""
         b = C.c_int32()

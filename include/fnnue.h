@@ -89,6 +89,12 @@ uint32_t fnnue_abi_version(void);
  * chain and exact EOF. */
 int fnnue_net_load(const char *path, fnnue_net **out);
 int fnnue_net_load_mem(const void *buf, size_t len, fnnue_net **out);
+/* Net identity ([ref] build.rs:7 pins nn-ad9b42354671.nnue; build.rs:100-112
+ * deletes a corrupt download): fnnue_net_load / fnnue_net_load_variant compute
+ * the SHA-256 of the file, and when its basename is nn-<12 lowercase hex>.nnue
+ * (upstream's naming: the first 12 hex digits of the digest) a mismatch fails
+ * with FNNUE_E_FORMAT.  digest: 32 bytes (also for nets loaded from memory). */
+int fnnue_net_sha256(const fnnue_net *net, uint8_t *digest);
 /* hd = TransformedFeatureDimensions (1024 for nn-ad9b42354671, [ref] build.rs:7). */
 int fnnue_net_info(const fnnue_net *net, uint32_t *hd, uint32_t *file_hash, const char **desc);
 void fnnue_net_free(fnnue_net *net);

@@ -508,3 +508,31 @@ def test_swar_rows_match_packed_rows(ev_cache, seed, hd, flags):
     with pytest.raises(F.FnnueError) as e:
         evw.set_swar(True)
     assert e.value.name == "FNNUE_E_ARCH"
+
+
+@pytest.mark.skipif(not os.environ.get("FNNUE_NET"), reason="set FNNUE_NET=<path to a real .nnue> to run")
+def test_real_net_file_matches_oracle():
+    """Opt-in: a real Stockfish net (e.g. nn-ad9b42354671.nnue, [ref] build.rs:7)
+    if one is ever placed on the box.  Loading checks its identity (SHA-256
+    prefix = name) and the structure-hash chain; then GPU == oracle over 200k
+    config-2 random-playout positions (from scratch) and 2,000 games' plies
+    (incremental CHAIN).  A match of both loaders on a real file pins the
+    recalled architecture constants."""
+    path = os.environ["FNNUE_NET"]
+    data = open(path, "rb").read()
+    net = F.Net.load(path)
+    ev = F.Evaluator(net, 0)
+    on = OracleNet(data)
+    try:
+        pos = F.random_playouts(1, 200_000, 0, 160, threads=8)
+        ps, po = ev.eval_positions(pos)
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert rc == 0 and np.array_equal(ps, ops) and np.array_equal(po, opo)
+        gpos, off = F.random_playouts(2, 2000, 0, 160, mode=N.PLAYOUT_PLIES, threads=8)
+        gs, go = ev.eval_groups(gpos, off, N.GROUP_CHAIN)
+        ops, opo, rc = on.eval_packed(gpos, threads=8)
+        assert rc == 0 and np.array_equal(gs, ops) and np.array_equal(go, opo)
+        print(json.dumps({"real_net": os.path.basename(path), "sha256": net.sha256(), "hd": net.info()[0],
+                          "positions": len(pos), "plies": len(gpos), "mismatches": 0}))
+    finally:
+        ev.close()

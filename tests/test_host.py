@@ -80,6 +80,54 @@ def test_net_file_roundtrip(tmp_path):
     assert F.Net.load(str(p)).info()[0] == 128
 
 
+@pytest.mark.parametrize("hd,flags", [(128, 0), (256, N.SYNTH_LEB128), (512, N.SYNTH_WRAP), (1024, 0)])
+def test_net_sha256_matches_hashlib(hd, flags):
+    """fnnue_net_sha256 (FIPS 180-4 restated in csrc/sha256.cpp) == hashlib on
+    files of several lengths (plain and LEB128 tensors: different tail blocks)."""
+    import hashlib
+    data = net_bytes(3, hd, flags)
+    assert F.Net.from_bytes(data).sha256() == hashlib.sha256(data).hexdigest()
+
+
+def test_net_identity_from_file_name(tmp_path):
+    """[ref] build.rs:7 pins nn-ad9b42354671.nnue; upstream names a net by the
+    first 12 hex digits of its SHA-256 and build.rs:100-112 deletes a corrupt
+    download.  A file whose nn-<12 hex>.nnue name matches its digest loads; a
+    mismatching one fails with FNNUE_E_FORMAT; other names make no claim."""
+    import hashlib
+    data = net_bytes(7, 128, 0)
+    digest = hashlib.sha256(data).hexdigest()
+    good = tmp_path / f"nn-{digest[:12]}.nnue"
+    good.write_bytes(data)
+    net = F.Net.load(str(good))
+    assert net.sha256() == digest and net.info()[0] == 128
+    wrong = "ad9b42354671" if digest[:12] != "ad9b42354671" else "000000000000"
+    bad = tmp_path / f"nn-{wrong}.nnue"
+    bad.write_bytes(data)
+    with pytest.raises(F.FnnueError) as e:
+        F.Net.load(str(bad))
+    assert e.value.name == "FNNUE_E_FORMAT" and wrong in str(e.value)
+    flipped = bytearray(data)
+    flipped[len(data) // 2] ^= 1  # one bit of the weights: same structure, different digest
+    corrupt = tmp_path / "sub"
+    corrupt.mkdir()
+    (corrupt / good.name).write_bytes(bytes(flipped))
+    with pytest.raises(F.FnnueError) as e:
+        F.Net.load(str(corrupt / good.name))
+    assert e.value.name == "FNNUE_E_FORMAT"
+    for other in ("nn-AD9B42354671.nnue", "nn-ad9b4235467.nnue", "custom.nnue", "nn-ad9b42354671.bin"):
+        (tmp_path / other).write_bytes(data)
+        assert F.Net.load(str(tmp_path / other)).sha256() == digest  # no identity claim in the name
+    vdata = F.synthesize_variant_net(2, 256, F.VARIANT_ATOMIC)
+    vd = hashlib.sha256(vdata).hexdigest()
+    (tmp_path / f"nn-{vd[:12]}.nnue").write_bytes(vdata)
+    assert F.Net.load_variant(str(tmp_path / f"nn-{vd[:12]}.nnue"), F.VARIANT_ATOMIC).sha256() == vd
+    (tmp_path / "nn-0123456789ab.nnue").write_bytes(vdata)
+    with pytest.raises(F.FnnueError) as e:
+        F.Net.load_variant(str(tmp_path / "nn-0123456789ab.nnue"), F.VARIANT_ATOMIC)
+    assert e.value.name == "FNNUE_E_FORMAT"
+
+
 @pytest.mark.parametrize("fen,counts", PERFT)
 def test_perft_known_answers(fen, counts):
     for depth, expect in enumerate(counts, start=1):
@@ -199,3 +247,10 @@ def test_accumulator_bound_decides_swar():
     assert 0 < b < 32768
     w = F.Net.from_bytes(F.synthesize_net(3, 1024, N.SYNTH_WRAP)).accumulator_bound()
     assert w >= 32768
+
+
+def test_playouts_accept_the_full_ply_range():
+    """max_plies = 2^32 - 1: the ply-count range is widened before the +1 (no
+    division by zero); games still end by mate, stalemate or the 50-move rule."""
+    pos = F.random_playouts(5, 2, 0, 2 ** 32 - 1, threads=1)
+    assert len(pos) == 2
