@@ -45,6 +45,15 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
                                uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
                                size_t off_cap, hipStream_t s);
 
+// Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub); synchronises s.
+hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s);
+
+// The same expansion for Fairy-Stockfish variants (vbuilder.hip, vboard.h):
+// crazyhouse / atomic FENs and UCI moves (drops "P@e4"), fnnue_vpos records.
+BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                                uint32_t ngames, bool children, fnnue_vpos* d_out, size_t cap, uint32_t* d_group_off,
+                                size_t off_cap, hipStream_t s);
+
 // Leaf count of perft(depth) summed over the frontier boards (1 <= depth <= 3).
 hipError_t perft_device(const std::vector<DBoard>& frontier, int depth, uint64_t* nodes);
 

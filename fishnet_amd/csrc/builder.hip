@@ -487,8 +487,10 @@ __global__ void perft_kernel(const DBoard* __restrict__ states, uint32_t n, unsi
   atomicAdd(total, (unsigned long long)perft_dev<D>(states[i]));
 }
 
+}  // namespace
+
 // Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub).
-hipError_t exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s) {
+hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s) {
   size_t tmp_bytes = 0;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, (int)n + 1, s);
   if (e != hipSuccess) return e;
@@ -499,8 +501,6 @@ hipError_t exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStr
   (void)hipFree(tmp);
   return e != hipSuccess ? e : e2;
 }
-
-}  // namespace
 
 DBoard to_dboard(const Board& h) {
   DBoard b{};
@@ -546,7 +546,7 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
   hipLaunchKernelGGL(count_plies_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
                      ngames, plies);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e);
-  if ((e = exclusive_scan(plies, ply_off, ngames, s)) != hipSuccess) return fail(e);
+  if ((e = builder_exclusive_scan(plies, ply_off, ngames, s)) != hipSuccess) return fail(e);
   uint32_t total_plies = 0;
   if ((e = hipMemcpy(&total_plies, ply_off + ngames, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
   if (!children) {
@@ -582,7 +582,7 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
     hipLaunchKernelGGL(count_children_kernel, dim3((total_plies + bs - 1) / bs), dim3(bs), 0, s, states,
                        total_plies, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
-    if ((e = exclusive_scan(cnt, coff, total_plies, s)) != hipSuccess) return fail(e);
+    if ((e = builder_exclusive_scan(cnt, coff, total_plies, s)) != hipSuccess) return fail(e);
     uint32_t total = 0;
     if ((e = hipMemcpy(&total, coff + total_plies, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
     R.n_out = total;

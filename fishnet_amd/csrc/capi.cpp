@@ -642,16 +642,17 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
   return FNNUE_OK;
 }
 
-int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint32_t* d_off, size_t ngroups,
-                             size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {
-  // The offsets stay on the device (no D2H, no stream drain, at any size): they
-  // are checked there (group_span_kernel, latched as FNNUE_E_ARG), and a call
-  // above one workspace is cut into chunks at fixed positions; a group cut by
-  // a chunk boundary restarts there with a refresh (results are identical).
-  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
-  if (ctx->variant != kVariantChess)
-    return fail(FNNUE_E_ARCH, "variant net: grouped evaluation is not supported for variant nets; use "
-                              "fnnue_eval_vpositions*");
+}  // extern "C"
+
+namespace {
+
+// Grouped evaluation on the device (chess or a variant feature set): the
+// offsets stay on the device (no D2H, no stream drain, at any size): they are
+// checked there (group_span_kernel, latched as FNNUE_E_ARG), and a call above
+// one workspace is cut into chunks at fixed positions; a group cut by a chunk
+// boundary restarts there with a refresh (results are identical).
+int eval_groups_device(fnnue_ctx* ctx, const void* d_pos, size_t pos_bytes, const uint32_t* d_off, size_t ngroups,
+                       size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {
   if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
   if (ngroups == 0) return npos == 0 ? FNNUE_OK : fail(FNNUE_E_ARG, "positions without groups");
   if (ngroups > 0xFFFFFFFFu || npos > 0xFFFFFFFFu) return fail(FNNUE_E_ARG, "batch too large");
@@ -661,32 +662,51 @@ int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint3
   int rc = order_workspace(ctx, s);
   if (rc) return rc;
   WorkspaceUse use{ctx, s};
-  const bool sliced = ctx->ft_impl == FNNUE_FT_SLICED;
+  const bool sliced = ctx->ft_impl == FNNUE_FT_SLICED || ctx->variant != kVariantChess;
   if (sliced && ((rc = ensure_seg(ctx)) || (rc = ensure_span(ctx, npos)))) return rc;
   HIP_TRY(launch_group_span(d_off, (uint32_t)ngroups, (uint32_t)npos, sliced ? ctx->seg.span : nullptr, true,
                             ctx->err, s),
           "group_span launch");
   const uint2* span = static_cast<const uint2*>(ctx->seg.span);
+  const char* pos = static_cast<const char*>(d_pos);
   for (size_t b = 0; b < npos; b += ctx->chunk) {
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, npos - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
     if ((rc = next_events(ctx, &ev))) return rc;
     if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
     if (sliced) {
-      HIP_TRY(launch_ft_segments(ctx->hd, d_pos + b, m, span + b, (uint32_t)b, mode, ctx->ptrs, ctx->plan, ctx->seg,
-                                 ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
+      HIP_TRY(launch_ft_segments(ctx->hd, ctx->variant, pos + b * pos_bytes, m, span + b, (uint32_t)b, mode,
+                                 ctx->ptrs, ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
               "ft_segments launch");
       rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, nullptr, ctx->plan.psqt_part, d_psqt + b);
     } else {
       if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
-      HIP_TRY(launch_ft_groups(ctx->hd, d_pos, d_off, (uint32_t)ngroups, (uint32_t)b, (uint32_t)(b + m), mode,
-                               ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
+      HIP_TRY(launch_ft_groups(ctx->hd, static_cast<const fnnue_pos*>(d_pos), d_off, (uint32_t)ngroups, (uint32_t)b,
+                               (uint32_t)(b + m), mode, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_groups launch");
       rc = run_chunk_tail(ctx, m, d_positional + b, s, ev);
     }
     if (rc) return rc;
   }
   return FNNUE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint32_t* d_off, size_t ngroups,
+                             size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant != kVariantChess) return fail(FNNUE_E_ARCH, "variant net: use fnnue_eval_vgroups*");
+  return eval_groups_device(ctx, d_pos, sizeof(fnnue_pos), d_off, ngroups, npos, mode, d_psqt, d_positional, stream);
+}
+
+int fnnue_eval_vgroups_device(fnnue_ctx* ctx, const fnnue_vpos* d_pos, const uint32_t* d_off, size_t ngroups,
+                              size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant == kVariantChess) return fail(FNNUE_E_ARCH, "chess net: use fnnue_eval_groups*");
+  return eval_groups_device(ctx, d_pos, sizeof(fnnue_vpos), d_off, ngroups, npos, mode, d_psqt, d_positional, stream);
 }
 
 int fnnue_eval_vpositions_device(fnnue_ctx* ctx, const fnnue_vpos* d_pos, size_t n, int32_t* d_psqt,
@@ -799,6 +819,34 @@ int fnnue_eval_groups(fnnue_ctx* ctx, const fnnue_pos* pos, size_t npos, const u
   HIP_TRY(hipMemcpyAsync(positional, ctx->d_positional, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
   HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
   return name_invalid(latched(ctx), pos, npos);
+}
+
+int fnnue_eval_vgroups(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t npos, const uint32_t* off, size_t ngroups,
+                       int mode, int32_t* psqt, int32_t* positional) {
+  if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
+  if (ctx->variant == kVariantChess) return fail(FNNUE_E_ARCH, "chess net: use fnnue_eval_groups*");
+  if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
+  if (ngroups == 0) return npos == 0 ? FNNUE_OK : fail(FNNUE_E_ARG, "positions without groups");
+  if (ngroups > 0xFFFFFFFFu || npos > 0xFFFFFFFFu) return fail(FNNUE_E_ARG, "batch too large");
+  if (!pos || !off || !psqt || !positional) return fail(FNNUE_E_ARG, "null buffer");
+  if (off[0] != 0) return fail(FNNUE_E_ARG, "off[0] must be 0");
+  for (size_t g = 0; g < ngroups; ++g)
+    if (off[g + 1] < off[g]) return fail(FNNUE_E_ARG, "group offsets must be non-decreasing");
+  if (off[ngroups] != npos) return fail(FNNUE_E_ARG, "off[ngroups] must equal npos");
+  DeviceGuard g(ctx->device);
+  int rc = ensure_stage(ctx, std::max<size_t>(npos, 1), ngroups + 1);
+  if (rc) return rc;
+  fnnue_vpos* d_vpos = reinterpret_cast<fnnue_vpos*>(ctx->d_pos);  // staging sized for fnnue_vpos
+  HIP_TRY(hipMemcpyAsync(d_vpos, pos, npos * sizeof(fnnue_vpos), hipMemcpyHostToDevice, ctx->stream), "H2D");
+  HIP_TRY(hipMemcpyAsync(ctx->d_off, off, (ngroups + 1) * 4, hipMemcpyHostToDevice, ctx->stream), "H2D");
+  rc = fnnue_eval_vgroups_device(ctx, d_vpos, ctx->d_off, ngroups, npos, mode, ctx->d_psqt, ctx->d_positional,
+                                 ctx->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(psqt, ctx->d_psqt, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+  HIP_TRY(hipMemcpyAsync(positional, ctx->d_positional, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+  HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+  if ((rc = latched(ctx)) == FNNUE_E_POSITION) return fail(rc, "invalid variant position in the batch");
+  return rc;
 }
 
 // ---- batch building ----

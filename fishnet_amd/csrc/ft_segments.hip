@@ -38,11 +38,19 @@
 //                 full lists (write_rows)
 //   ft_segments   (unit, slice) workgroups, XCD-aware, tile in LDS
 // then stack_kernel over x / bucket / psqt_part in position order.
+//
+// The same machinery runs the Fairy-Stockfish variant feature sets (64 king
+// blocks, crazyhouse pocket rows): a feature set Fs supplies the position
+// record, its decode, king blocks, feature rows and the tile geometry.  A
+// variant ply's delta also carries its pocket changes as row adds / removes
+// (a capture adds the captured piece's next hand row, a drop removes the
+// dropped piece's last one); atomic explosions exceed two removed rows and
+// refresh.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
 
-#include "sliced_common.h"
+#include "variant_common.h"
 
 namespace fnnue {
 
@@ -51,7 +59,66 @@ namespace {
 constexpr uint32_t kSlotMask = 0xFFFFFF;  // item record x: slot | half << 24 | bucket << 25
 constexpr uint32_t kRowMask = 0x1FFFFFF;  // delta record x: (2 * slot + half) | bucket << 25
 // A segment item is a whole run of positions walked serially, so units are
-// cut by positions (kSegUnitPlies, plan_scan_kernel) rather than by items.
+// cut by positions (kSegUnitPlies, plan_scan_kernel_t) rather than by items.
+
+// Feature sets.  Dec: the lane decode (board b, list length + 1 = nfeat, ok).
+// kNone: 16 * the tile's first zero row (unused delta slots, sentinel).
+struct ChessFs {
+  using Pos = fnnue_pos;
+  using G = ChessGeom;
+  static constexpr int KB = 32;
+  static constexpr bool kHand = false;
+  static constexpr uint32_t kNone = 16u * G::kRows;
+  struct Dec {
+    LaneBoard b;
+    uint32_t hand[10];
+    int nfeat;
+    bool ok;
+  };
+  __device__ static __forceinline__ Dec decode(const Pos* p) {
+    Dec d;
+    d.b = lane_decode(p);
+    d.nfeat = d.b.cnt;
+    d.ok = d.b.ok;
+    return d;
+  }
+  __device__ static __forceinline__ int block(int c, int ksq) { return king_block(c, ksq); }
+  __device__ static __forceinline__ uint32_t board_entry(int c, int s, int pc, int ksq, int kb) {
+    return 16u * (uint32_t)(make_index(c, s, pc, ksq) - kRowsPerBlock * kb);
+  }
+  __device__ static __forceinline__ void write_list(const Dec& d, int c, uint32_t it, const uint32_t* ctr,
+                                                    uint32_t* mine, uint16_t* flist) {
+    write_rows(d.b, c, c ? d.b.bk : d.b.wk, it, ctr, mine, flist);
+  }
+};
+
+template <int V>  // kVariantCrazyhouse / kVariantAtomic
+struct VariantFs {
+  using Pos = fnnue_vpos;
+  static constexpr int R = (int)variant_rows(V);
+  using G = VariantGeom<R>;
+  static constexpr int KB = 64;
+  static constexpr bool kHand = V == kVariantCrazyhouse;
+  static constexpr uint32_t kNone = 16u * R;
+  using Dec = VariantBoard;
+  __device__ static __forceinline__ Dec decode(const Pos* p) { return vdecode(p, kHand); }
+  __device__ static __forceinline__ int block(int c, int ksq) { return vblock(c, ksq); }
+  __device__ static __forceinline__ uint32_t board_entry(int c, int s, int pc, int, int) {
+    return 16u * vboard_row(c, s, pc);
+  }
+  __device__ static __forceinline__ void write_list(const Dec& d, int c, uint32_t it, const uint32_t* ctr,
+                                                    uint32_t* mine, uint16_t* flist) {
+    const int kb = vblock(c, c ? d.b.bk : d.b.wk);
+    vwrite_rows<R>(d, c, it, (it - ctr[kVOff + kb * 33]) & 1u, mine, flist);
+  }
+};
+
+// Counter layout of a feature set's plan (plan_scan_kernel_t<KB>).
+template <class Fs>
+struct SegCtr {
+  static constexpr int kIB = Fs::KB * 33, kB = kIB + kPosBins, kOff = kB, kCur = 2 * kB;
+  static constexpr size_t kWords = 3 * kB + 16;
+};
 
 // Each position's group span {first, end}, absolute positions of the whole
 // call, written once per call by group_span_kernel (one wave per group fills
@@ -89,17 +156,15 @@ __device__ __forceinline__ uint2 group_range(const uint2* __restrict__ span, uin
   return make_uint2(min(a, i), min(max(b, i + 1), n));
 }
 
-__device__ __forceinline__ uint32_t feature_entry(int persp, int s, int pc, int ksq, int kb) {
-  return 16u * (uint32_t)(make_index(persp, s, pc, ksq) - kRowsPerBlock * kb);
-}
-
 // Refresh flags r0 / r1 and delta records of position i (both perspectives).
-__device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos, uint32_t n,
+template <class Fs>
+__device__ __forceinline__ void seg_delta_one(const typename Fs::Pos* __restrict__ pos, uint32_t n,
                                               const uint2* __restrict__ span, uint32_t sbase, int star,
                                               uint32_t* __restrict__ ref,
                                               uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
                                               uint32_t* __restrict__ err, uint32_t i, uint32_t& r0, uint32_t& r1) {
-  const LaneBoard B = lane_decode(pos + i);
+  using Dec = typename Fs::Dec;
+  const Dec B = Fs::decode(pos + i);
   if (!B.ok) {
     // no item, no accumulator; counted as a refresh so that STAR ranks skip it
     bucket[i] = 0xFF;
@@ -108,46 +173,62 @@ __device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos,
     atomicOr(err, 1u);
     return;
   }
-  const uint32_t bk = (uint32_t)(B.cnt - 1) >> 2;
+  const uint32_t bk = (uint32_t)(B.b.cnt - 1) >> 2;  // board pieces
   bucket[i] = (uint8_t)bk;
   const uint32_t first = group_range(span, i, n, sbase).x;
   const bool has_base = i > first;
-  LaneBoard A;
+  Dec A;
   bool base_ok = false;
   uint64_t changed = 0;
   if (has_base) {
-    A = lane_decode(pos + (star ? first : i - 1));
+    A = Fs::decode(pos + (star ? first : i - 1));
     base_ok = A.ok;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      changed |= (uint64_t)nibble_bits(~zero_nibbles(A.w[k] ^ B.w[k]) & 0x88888888u) << (8 * k);
+      changed |= (uint64_t)nibble_bits(~zero_nibbles(A.b.w[k] ^ B.b.w[k]) & 0x88888888u) << (8 * k);
   }
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    const int ksq = c ? B.bk : B.wk;
-    bool refresh = !base_ok || (c ? A.bk : A.wk) != ksq || __popcll(changed) > 4;
-    uint32_t rem[2] = {kNoEntry, kNoEntry}, add[2] = {kNoEntry, kNoEntry};
+    const int ksq = c ? B.b.bk : B.b.wk;
+    bool refresh = !base_ok || (c ? A.b.bk : A.b.wk) != ksq || __popcll(changed) > 4;
+    uint32_t rem[2] = {Fs::kNone, Fs::kNone}, add[2] = {Fs::kNone, Fs::kNone};
     if (!refresh) {
-      const int kb = king_block(c, ksq);
+      const int kb = Fs::block(c, ksq);
       int nr = 0, na = 0;
       for (uint64_t m = changed; m; m &= m - 1) {
         const int s = __builtin_ctzll(m);
-        const int was = nibble_at(A.w, s), now = nibble_at(B.w, s);
+        const int was = nibble_at(A.b.w, s), now = nibble_at(B.b.w, s);
         if (was) {
-          if (nr < 2) rem[nr] = feature_entry(c, s, was, ksq, kb);
+          if (nr < 2) rem[nr] = Fs::board_entry(c, s, was, ksq, kb);
           ++nr;
         }
         if (now) {
-          if (na < 2) add[na] = feature_entry(c, s, now, ksq, kb);
+          if (na < 2) add[na] = Fs::board_entry(c, s, now, ksq, kb);
           ++na;
         }
       }
-      refresh = nr > 2 || na > 2;  // never for a legal move; arbitrary groups refresh
+      if constexpr (Fs::kHand) {
+        // pocket slot j holding `was` pieces before and `now` after: the rows
+        // of its pieces was .. now - 1 are added, now .. was - 1 removed
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          const uint32_t was = A.hand[j], now = B.hand[j];
+          for (uint32_t k = now; k < was && nr <= 2; ++k) {
+            if (nr < 2) rem[nr] = 16u * vhand_row(c, j, k);
+            ++nr;
+          }
+          for (uint32_t k = was; k < now && na <= 2; ++k) {
+            if (na < 2) add[na] = 16u * vhand_row(c, j, k);
+            ++na;
+          }
+        }
+      }
+      refresh = nr > 2 || na > 2;  // never for a legal chess move; explosions / arbitrary groups refresh
     }
     ref[c * n + i] = refresh ? 1u : 0u;
     (c ? r1 : r0) = refresh ? 1u : 0u;
     if (!refresh) {
-      const uint32_t half = B.stm == c ? 0u : 1u;
+      const uint32_t half = B.b.stm == c ? 0u : 1u;
       dtmp[c * n + i] = make_uint4((2u * i + half) | bk << 25, rem[0] | rem[1] << 16, add[0] | add[1] << 16, 0u);
     }
   }
@@ -155,7 +236,8 @@ __device__ __forceinline__ void seg_delta_one(const fnnue_pos* __restrict__ pos,
 
 // The first kernel of a chunk's plan: block 0 also zeroes the counter block
 // (read by seg_count / plan_scan / seg_scatter) instead of a memset launch.
-__global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+template <class Fs>
+__global__ __launch_bounds__(256) void seg_delta_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
                                                         const uint2* __restrict__ span, uint32_t sbase, int star,
                                                         uint32_t* __restrict__ ref,
                                                         uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
@@ -165,7 +247,7 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const fnnue_pos* __restr
     for (uint32_t k = threadIdx.x; k < ctr_words; k += blockDim.x) ctr[k] = 0;
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   uint32_t r0 = 0, r1 = 0;
-  if (i < n) seg_delta_one(pos, n, span, sbase, star, ref, dtmp, bucket, err, i, r0, r1);
+  if (i < n) seg_delta_one<Fs>(pos, n, span, sbase, star, ref, dtmp, bucket, err, i, r0, r1);
   // refresh counts of this block's 256 positions, per perspective (seg_scan_blocks)
   const int c0 = __syncthreads_count((int)r0), c1 = __syncthreads_count((int)r1);
   if (threadIdx.x == 0) {
@@ -232,6 +314,7 @@ __global__ __launch_bounds__(256) void seg_items_scan_kernel(uint32_t n, const u
 //   refreshes.
 // * any other position places its delta record at root + rank, so that a
 //   segment's records are contiguous.
+template <class Fs>
 __global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, uint32_t sbase,
                                                         int star,
                                                         const uint8_t* __restrict__ bucket,
@@ -243,7 +326,7 @@ __global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2*
   // Record 2n, read by items past the end of their segment: no rows, x row 2n
   // and bucket 0, i.e. x and PSQT stores just past the launch's buffer ranges
   // (dropped by the hardware), so the walk needs no liveness masking.
-  if (j == 0) drec[2 * n] = make_uint4(2 * n, kNoEntry | kNoEntry << 16, kNoEntry | kNoEntry << 16, 0u);
+  if (j == 0) drec[2 * n] = make_uint4(2 * n, Fs::kNone | Fs::kNone << 16, Fs::kNone | Fs::kNone << 16, 0u);
   if (j >= 2 * n) return;
   const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
   if (ref[j]) {
@@ -272,65 +355,70 @@ __global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2*
   drec[c * n + r + rank] = dtmp[j];
 }
 
-__device__ __forceinline__ uint32_t seg_key(const LaneBoard& b, int c, uint32_t L) {
-  return (uint32_t)king_block(c, c ? b.bk : b.wk) * 33u + seg_len_bin(L);
+template <class Fs>
+__device__ __forceinline__ uint32_t seg_key(const typename Fs::Dec& d, int c, uint32_t L) {
+  return (uint32_t)Fs::block(c, c ? d.b.bk : d.b.wk) * 33u + seg_len_bin(L);
 }
 
 // Both sort kernels run one thread per item k < cref[2n] (refresh of
 // perspective k >= cref[n]); invalid positions are refreshes with len 0.
-__global__ __launch_bounds__(1024) void seg_count_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+template <class Fs>
+__global__ __launch_bounds__(1024) void seg_count_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
                                                          const uint32_t* __restrict__ cref,
                                                          const uint32_t* __restrict__ ipos,
                                                          const uint32_t* __restrict__ len,
                                                          uint32_t* __restrict__ ctr) {
-  __shared__ uint32_t h[kItemBins];
-  for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) h[i] = 0;
+  constexpr int kIB = SegCtr<Fs>::kIB;
+  __shared__ uint32_t h[kIB];
+  for (int i = threadIdx.x; i < kIB; i += blockDim.x) h[i] = 0;
   __syncthreads();
   const uint32_t K = cref[2 * n], K0 = cref[n];
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
     const uint32_t c = k >= K0 ? 1u : 0u, i = ipos[k], L = len[c * n + i];
-    if (L) atomicAdd(&h[seg_key(lane_decode(pos + i), (int)c, L)], 1u);
+    if (L) atomicAdd(&h[seg_key<Fs>(Fs::decode(pos + i), (int)c, L)], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kItemBins; i += blockDim.x)
-    if (h[i]) atomicAdd(&ctr[kCnt + i], h[i]);
+  for (int i = threadIdx.x; i < kIB; i += blockDim.x)
+    if (h[i]) atomicAdd(&ctr[i], h[i]);
 }
 
 // Sorted item record: {root | half << 24 | bucket << 25, length, perspective,
-// piece count}; full feature list of the root as in the sliced plan.
-__global__ __launch_bounds__(1024) void seg_scatter_kernel(const fnnue_pos* __restrict__ pos, uint32_t n,
+// list length + 1}; full feature list of the root as in the sliced plan.
+template <class Fs>
+__global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
                                                            const uint32_t* __restrict__ cref,
                                                            const uint32_t* __restrict__ ipos,
                                                            const uint32_t* __restrict__ len,
                                                            uint32_t* __restrict__ ctr, uint4* __restrict__ items,
                                                            uint16_t* __restrict__ flist) {
-  __shared__ uint32_t lcnt[kItemBins];
-  __shared__ uint32_t lbase[kItemBins];
-  __shared__ uint32_t lists[1024 * kListStrideWords];  // write_rows staging, one row per lane
+  constexpr int kIB = SegCtr<Fs>::kIB;
+  __shared__ uint32_t lcnt[kIB];
+  __shared__ uint32_t lbase[kIB];
+  __shared__ uint32_t lists[1024 * kListStrideWords];  // list staging, one row per lane
   const uint32_t K = cref[2 * n], K0 = cref[n];
   if (blockIdx.x * blockDim.x >= K) return;  // workgroup-uniform
-  for (int i = threadIdx.x; i < kItemBins; i += blockDim.x) lcnt[i] = 0;
+  for (int i = threadIdx.x; i < kIB; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t c = k >= K0 ? 1u : 0u, i = k < K ? ipos[k] : 0u;
   const uint32_t L = k < K ? len[c * n + i] : 0u;
   const bool live = L != 0;
-  LaneBoard b;
+  typename Fs::Dec d;
   uint32_t key = 0, rk = 0;
   if (live) {
-    b = lane_decode(pos + i);
-    key = seg_key(b, (int)c, L);
+    d = Fs::decode(pos + i);
+    key = seg_key<Fs>(d, (int)c, L);
     rk = atomicAdd(&lcnt[key], 1u);
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < kItemBins; t += blockDim.x)
-    lbase[t] = lcnt[t] ? atomicAdd(&ctr[kCur + t], lcnt[t]) : 0;
+  for (int t = threadIdx.x; t < kIB; t += blockDim.x)
+    lbase[t] = lcnt[t] ? atomicAdd(&ctr[SegCtr<Fs>::kCur + t], lcnt[t]) : 0;
   __syncthreads();
   if (!live) return;
   const uint32_t slot = lbase[key] + rk;
-  const uint32_t half = b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(b.cnt - 1) >> 2;
-  items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)b.cnt);
-  write_rows(b, (int)c, c ? b.bk : b.wk, slot, ctr, lists + threadIdx.x * kListStrideWords, flist);
+  const uint32_t half = d.b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(d.b.cnt - 1) >> 2;
+  items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)d.nfeat);
+  Fs::write_list(d, (int)c, slot, ctr, lists + threadIdx.x * kListStrideWords, flist);
 }
 
 struct SegFetch {
@@ -404,19 +492,27 @@ __device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4&
 // Then the wave walks the longest segment of the pass; finished items turn
 // their rows into the zero row and their stores out of range (dropped).
 constexpr int kDbufStride = 9;  // records per item in the per-wave LDS buffer (8 + 1 padding)
+// One LDS buffer per wave serves both the pass's feature lists (64 x 8 B) and
+// the walk's delta records (8 items x kDbufStride x 16 B): a wave uses them
+// one after the other and its LDS operations complete in order, so they share
+// the bytes (the crazyhouse tile and its PSQT tile then still fit in 160 KB).
+// may_alias types and compiler barriers keep the two views ordered.
+constexpr int kWaveBufU4 = 8 * kDbufStride;
+typedef uint2 lds_u2 __attribute__((may_alias));
+typedef uint4 lds_u4 __attribute__((may_alias));
 
-template <int HD, bool kStar, bool kPsqt, bool kSwar>
-__device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ lb, int lane, int it_in_wave, int s,
+template <int HD, bool kStar, bool kPsqt, bool kSwar, uint32_t kNone>
+__device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ wbuf, int lane, int it_in_wave, int s,
                                          int q, uint32_t n, const char* lbase, u16x4 b_lo, u16x4 b_hi, int krow,
                                          const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
-                                         __amdgpu_buffer_rsrc_t x_rsrc, __amdgpu_buffer_rsrc_t drec_rsrc,
-                                         uint4* __restrict__ dbuf) {
+                                         __amdgpu_buffer_rsrc_t x_rsrc, __amdgpu_buffer_rsrc_t drec_rsrc) {
   const uint4 rec = f.rec;
   const uint32_t maxn = __builtin_amdgcn_readfirstlane(wave_max_u32(rec.w));
   const uint32_t maxL = __builtin_amdgcn_readfirstlane(wave_max_u32(rec.y));
-  lb[lane] = f.lst;
+  asm volatile("" ::: "memory");  // the previous pass's record reads come first
+  reinterpret_cast<lds_u2*>(wbuf)[lane] = f.lst;
   uint32_t e[16];
-  const uint4* my = reinterpret_cast<const uint4*>(lb) + 4 * it_in_wave;
+  const lds_u4* my = reinterpret_cast<const lds_u4*>(wbuf) + 4 * it_in_wave;
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const uint4 v = my[m];
@@ -460,7 +556,8 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
   // 9 records of stride per item (one padding record): the two items of a
   // ds_read_b96 lane group ({0-3,20-23}: items 0 and 1; banks (a/4) mod 32)
   // then read records 144 B apart, 4 banks, instead of 128 B = the same banks.
-  uint4* db = dbuf + kDbufStride * it_in_wave;
+  asm volatile("" ::: "memory");  // this pass's list reads come first
+  lds_u4* db = reinterpret_cast<lds_u4*>(wbuf) + kDbufStride * it_in_wave;
   const uint32_t nb = __builtin_amdgcn_readfirstlane((maxL - 1 + 7) / 8);  // batches, wave-uniform
   constexpr int kAhead = 1;  // batches of records in flight ahead of the current one (2: no gain, r01)
   uint4 next[kAhead];
@@ -497,14 +594,14 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint2* __restrict__ 
     next[kAhead - 1] = fetch(8 * (b + kAhead) + 1 + q);
     db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
     // lane q of an item holds record 8b+1+q: any with a second add?
-    if (__ballot((batch.z >> 16) != kNoEntry))
+    if (__ballot((batch.z >> 16) != kNone))
       run_batch(std::true_type{});
     else
       run_batch(std::false_type{});
   }
 }
 
-template <int HD, bool kStar, bool kSwar>
+template <int HD, bool kStar, bool kSwar, class Fs>
 __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restrict__ tiles,
                                                            const int16_t* __restrict__ ftb,
                                                            const uint32_t* __restrict__ ctr,
@@ -516,17 +613,19 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
                                                            int32_t* __restrict__ psqt_part,
                                                            uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
+  using G = typename Fs::G;
+  constexpr int kTileU4 = G::kTileU4;
   __shared__ uint4 img[kTileU4];
-  __shared__ int32_t ptile[kTileRows * kPsqtBuckets];
-  __shared__ uint2 lbuf[16][64];
-  __shared__ uint4 dbuf[16][8 * kDbufStride];  // per wave: 8 positions' delta records of its 8 items
+  __shared__ int32_t ptile[G::kTileRows * kPsqtBuckets];
+  __shared__ uint4 wbufs[16][kWaveBufU4];  // per wave: a pass's lists, then its delta records
   __shared__ uint32_t claim;  // next pass of the unit to hand out
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   int it_in_wave, q;
   lane_item(lane, it_in_wave, q);
   constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
-  constexpr int kPtileU4 = kTileRows * kPsqtBuckets / 4, kPtileRealU4 = kRowsPerBlock * kPsqtBuckets / 4;
+  constexpr int kPtileU4 = G::kTileRows * kPsqtBuckets / 4, kPtileRealU4 = G::kRows * kPsqtBuckets / 4;
+  static_assert(kPtileU4 <= 2048, "PSQT tile loads: two per thread");
   // Buffer ranges are this launch's exact extents (x: n rows of HD bytes,
   // < 2^31; psqt_part: 2n words; drec: 2n + 1 records, the last the sentinel
   // record 2n).  Items past their segment's end read the sentinel, whose x row
@@ -542,7 +641,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(flist), 0, kBufferAll, kBufferFlags);
   const __amdgpu_buffer_rsrc_t drec_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n + 16), kBufferFlags);
-  uint2* lb = lbuf[wv];
+  uint4* wb = wbufs[wv];
   // Grid-stride over (unit, slice) pairs: the unit count is known only on the
   // device and its bound (seg_max_units) is far above typical counts.  The
   // grid is a multiple of 8 * S, so every pair keeps its XCD-aware mapping.
@@ -560,15 +659,15 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
 #pragma unroll
     for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
     uint4 pt[2];
-    const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * kRowsPerBlock * kPsqtBuckets);
+    const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * G::kRows * kPsqtBuckets);
     if (s == 0) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
     }
     u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
     u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
-    const int krow = king_row(u.x);
-    const char* lbase = reinterpret_cast<const char*>(img) + kPlaneBytes * q;
+    const int krow = G::king_row(u.x);
+    const char* lbase = reinterpret_cast<const char*>(img) + G::kPlaneBytes * q;
     const int last = u.z - 1;
     // Passes are handed out longest first (items are sorted by length bin, so
     // from the unit's end backwards), the next one claimed from an LDS counter
@@ -614,17 +713,17 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       const int next = pass_base(kp);
       fa = fetch_seg(items_rsrc, flist_rsrc, next, last, lane, it_in_wave);
       if (s == 0)
-        seg_pass<HD, kStar, true, kSwar>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile,
-                                         psqt_rsrc, x_rsrc, drec_rsrc, dbuf[wv]);
+        seg_pass<HD, kStar, true, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
+                                                    ptile, psqt_rsrc, x_rsrc, drec_rsrc);
       else
-        seg_pass<HD, kStar, false, kSwar>(cur, lb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow, ptile,
-                                          psqt_rsrc, x_rsrc, drec_rsrc, dbuf[wv]);
+        seg_pass<HD, kStar, false, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
+                                                     ptile, psqt_rsrc, x_rsrc, drec_rsrc);
       base = next;
     }
   }
 }
 
-template <int HD>
+template <int HD, class Fs>
 hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& net, uint32_t n, bool star,
                          uint8_t* x, uint32_t max_units, hipStream_t stream) {
   constexpr int S = HD / 64;
@@ -636,9 +735,40 @@ hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& n
                        P.psqt_part, x);
   };
   if (star)
-    P.swar ? launch(ft_segments_kernel<HD, true, true>) : launch(ft_segments_kernel<HD, true, false>);
+    P.swar ? launch(ft_segments_kernel<HD, true, true, Fs>) : launch(ft_segments_kernel<HD, true, false, Fs>);
   else
-    P.swar ? launch(ft_segments_kernel<HD, false, true>) : launch(ft_segments_kernel<HD, false, false>);
+    P.swar ? launch(ft_segments_kernel<HD, false, true, Fs>) : launch(ft_segments_kernel<HD, false, false, Fs>);
+  return hipGetLastError();
+}
+
+// The plan of one chunk for feature set Fs (see the file comment), then the
+// dispatch of the main kernel over the net width.
+template <class Fs>
+hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, uint32_t sbase, bool star,
+                      const SlicedPlan& P, const SegPlan& G, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
+  hipError_t e;
+  const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
+  if (g1 > kMaxScanBlocks) return hipErrorInvalidValue;
+  uint32_t* bsum = static_cast<uint32_t*>(G.scan_temp);
+  hipLaunchKernelGGL(seg_delta_kernel<Fs>, dim3(g1), dim3(bs), 0, stream, pos, n, sp, sbase, star ? 1 : 0, G.ref,
+                     (uint4*)G.dtmp, bucket, err, bsum, P.ctr, (uint32_t)SegCtr<Fs>::kWords);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // cref = exclusive scan of ref (reduce in seg_delta, scan of the block sums, local scans)
+  hipLaunchKernelGGL(seg_scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, bsum, g1, n, G.cref);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_items_scan_kernel, dim3(g1, 2), dim3(256), 0, stream, n, G.ref, bsum, G.cref, G.ipos);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_place_kernel<Fs>, dim3(g2), dim3(bs), 0, stream, n, sp, sbase, star ? 1 : 0, bucket, G.ref,
+                     G.cref, G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  uint32_t cb = (2 * n + 1023) / 1024;
+  if (cb > 256) cb = 256;
+  hipLaunchKernelGGL(seg_count_kernel<Fs>, dim3(cb), dim3(1024), 0, stream, pos, n, G.cref, G.ipos, G.len, P.ctr);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(plan_scan_kernel_t<Fs::KB>, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(seg_scatter_kernel<Fs>, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.cref,
+                     G.ipos, G.len, P.ctr, (uint4*)G.items, P.flist);
   return hipGetLastError();
 }
 
@@ -646,7 +776,7 @@ hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& n
 
 // units close at kSegUnitPlies positions (>= 1 item each) or kUnitItems items;
 // a unit holding fewer than kSegUnitPlies / 160 items is its king block's last
-uint32_t seg_max_units(uint32_t chunk) { return 32 + (2 * chunk + kSegUnitPlies / 160 - 1) / (kSegUnitPlies / 160); }
+uint32_t seg_max_units(uint32_t chunk) { return 64 + (2 * chunk + kSegUnitPlies / 160 - 1) / (kSegUnitPlies / 160); }
 
 // the per-block refresh counts of seg_delta, two perspectives
 size_t seg_scan_temp_bytes(uint32_t chunk) { return (size_t)8 * ((chunk + 255) / 256 + 1); }
@@ -672,41 +802,42 @@ hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npo
   return hipGetLastError();
 }
 
-hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const void* span, uint32_t sbase,
+hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase,
                               int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
                               uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid) {
   if (n == 0) return hipSuccess;
   const bool star = mode == FNNUE_GROUP_STAR;
-  hipError_t e;
-  const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
-  if (g1 > kMaxScanBlocks) return hipErrorInvalidValue;
   const uint2* sp = static_cast<const uint2*>(span);
-  uint32_t* bsum = static_cast<uint32_t*>(G.scan_temp);
-  hipLaunchKernelGGL(seg_delta_kernel, dim3(g1), dim3(bs), 0, stream, pos, n, sp, sbase, star ? 1 : 0, G.ref,
-                     (uint4*)G.dtmp, bucket, err, bsum, P.ctr, (uint32_t)sliced_ctr_words());
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  // cref = exclusive scan of ref (reduce in seg_delta, scan of the block sums, local scans)
-  hipLaunchKernelGGL(seg_scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, bsum, g1, n, G.cref);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_items_scan_kernel, dim3(g1, 2), dim3(256), 0, stream, n, G.ref, bsum, G.cref, G.ipos);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_place_kernel, dim3(g2), dim3(bs), 0, stream, n, sp, sbase, star ? 1 : 0, bucket, G.ref,
-                     G.cref, G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  uint32_t cb = (2 * n + 1023) / 1024;
-  if (cb > 256) cb = 256;
-  hipLaunchKernelGGL(seg_count_kernel, dim3(cb), dim3(1024), 0, stream, pos, n, G.cref, G.ipos, G.len, P.ctr);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_scatter_kernel, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.cref, G.ipos,
-                     G.len, P.ctr, (uint4*)G.items, P.flist);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (mid && (e = hipEventRecord(mid, stream)) != hipSuccess) return e;
   const uint32_t mu = seg_max_units(n);
-#define CALL(H) ft_segments_t<H>(G, P, net, n, star, x, mu, stream)
-  FNNUE_HD_DISPATCH(hd, CALL)
+  hipError_t e;
+  auto mark = [&]() { return mid ? hipEventRecord(mid, stream) : hipSuccess; };
+  if (variant == kVariantChess) {
+    if ((e = seg_plan_t<ChessFs>(static_cast<const fnnue_pos*>(pos), n, sp, sbase, star, P, G, bucket, err, stream)) !=
+            hipSuccess ||
+        (e = mark()) != hipSuccess)
+      return e;
+#define CALL(H) ft_segments_t<H, ChessFs>(G, P, net, n, star, x, mu, stream)
+    FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
+  }
+  const fnnue_vpos* vp = static_cast<const fnnue_vpos*>(pos);
+#define FNNUE_VSEG(V)                                                                                      \
+  {                                                                                                        \
+    using Fs = VariantFs<V>;                                                                               \
+    if ((e = seg_plan_t<Fs>(vp, n, sp, sbase, star, P, G, bucket, err, stream)) != hipSuccess ||           \
+        (e = mark()) != hipSuccess)                                                                        \
+      return e;                                                                                            \
+    switch (hd) {                                                                                          \
+      case 256: return ft_segments_t<256, Fs>(G, P, net, n, star, x, mu, stream);                          \
+      case 512: return ft_segments_t<512, Fs>(G, P, net, n, star, x, mu, stream);                          \
+      case 1024: return ft_segments_t<1024, Fs>(G, P, net, n, star, x, mu, stream);                        \
+      default: return hipErrorInvalidValue;                                                                \
+    }                                                                                                      \
+  }
+  if (variant == kVariantCrazyhouse) FNNUE_VSEG(kVariantCrazyhouse)
+  if (variant == kVariantAtomic) FNNUE_VSEG(kVariantAtomic)
+#undef FNNUE_VSEG
+  return hipErrorInvalidValue;
 }
 
 }  // namespace fnnue

@@ -343,7 +343,7 @@ hipError_t launch_sliced_plan(const fnnue_pos* pos, uint32_t n, const SlicedPlan
   if (blocks > 256) blocks = 256;
   hipLaunchKernelGGL(plan_count_kernel, dim3(blocks), dim3(1024), 0, stream, pos, n, P.ctr, err);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
+  hipLaunchKernelGGL(plan_scan_kernel_t<32>, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, (uint32_t)kUnitItems);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(plan_scatter_kernel, dim3((n + kScatterPositions - 1) / kScatterPositions), dim3(kScatterPositions), 0, stream,
                      pos, n, P.ctr, P.items, P.flist, P.perm, bucket, psqt);

@@ -83,6 +83,10 @@ void ctx_destroy(fnnue_ctx* c);
 int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant);
 // Derives the LDS-tile layout of the FT weights from the (just written) image.
 int finish_upload(fnnue_ctx* c);
+// Grow-only host-API staging: positions (sized for fnnue_vpos) + outputs, offsets.
+int ensure_stage(fnnue_ctx* c, size_t npos, size_t noff);
+// Grow-only staging of a batch builder's input text and offsets.
+int ensure_builder_input(fnnue_ctx* c, size_t bytes);
 // Reads and clears the latched device error word.
 int latched(fnnue_ctx* c);
 // The device's position rule on the host (one king per side, <= 32 pieces, valid codes, stm 0/1).

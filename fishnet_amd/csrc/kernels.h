@@ -120,7 +120,9 @@ hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npo
 // One chunk: positions pos[0, n) = the call's positions [sbase, sbase + n),
 // span = the call's span table + sbase.  Groups cut by the chunk's edges are
 // clamped to it (their first in-chunk position refreshes).
-hipError_t launch_ft_segments(uint32_t hd, const fnnue_pos* pos, uint32_t n, const void* span, uint32_t sbase,
+// variant: kVariantChess (pos = fnnue_pos) or a Fairy-Stockfish feature set
+// (pos = fnnue_vpos; hd 256 / 512 / 1024; P.tiles / counters of that set).
+hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase,
                               int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
                               uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid = nullptr);
 

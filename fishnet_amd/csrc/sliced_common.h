@@ -157,19 +157,25 @@ __host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
 }
 
 // One workgroup of 1024 threads.  unit_items = 0: segment units (see
-// kSegUnitPlies) instead of fixed-size ones.
-__global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel(uint32_t* __restrict__ ctr, int4* __restrict__ units,
-                                                         uint32_t unit_items) {
-  __shared__ uint32_t s[kBins];
+// kSegUnitPlies) instead of fixed-size ones.  KB king blocks (32: chess; 64:
+// the variant feature sets), counters laid out as KB * 33 item bins + 9
+// position bins, then offsets, cursors and the unit count (kCnt / kOff / kCur
+// / kNUnits for KB = 32, kV* for 64).
+template <int KB>
+__global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel_t(uint32_t* __restrict__ ctr,
+                                                                                  int4* __restrict__ units,
+                                                                                  uint32_t unit_items) {
+  constexpr int kIB = KB * 33, kB = kIB + kPosBins, kO = kB, kC = 2 * kB, kNU = 3 * kB;
+  __shared__ uint32_t s[kB];
   __shared__ uint32_t part[1024];
   const int t = threadIdx.x;
   // Exclusive scan of the item bins and, separately, of the position bins.
-  constexpr int per = (kBins + 1023) / 1024;
+  constexpr int per = (kB + 1023) / 1024;
   uint32_t local[per];
   uint32_t sum = 0;
   for (int k = 0; k < per; ++k) {
     const int i = t * per + k;
-    local[k] = (i < kItemBins) ? ctr[kCnt + i] : 0;
+    local[k] = (i < kIB) ? ctr[i] : 0;
     sum += local[k];
   }
   part[t] = sum;
@@ -183,34 +189,37 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
   uint32_t run = part[t] - sum;
   for (int k = 0; k < per; ++k) {
     const int i = t * per + k;
-    if (i < kItemBins) s[i] = run;
+    if (i < kIB) s[i] = run;
     run += local[k];
   }
   if (t == 0) {
     uint32_t r = 0;
     for (int b = 0; b < kPosBins; ++b) {
-      s[kItemBins + b] = r;
-      r += ctr[kCnt + kItemBins + b];
+      s[kIB + b] = r;
+      r += ctr[kIB + b];
     }
   }
   __syncthreads();
-  for (int i = t; i < kBins; i += 1024) {
-    ctr[kOff + i] = s[i];
-    ctr[kCur + i] = s[i];
+  for (int i = t; i < kB; i += 1024) {
+    ctr[kO + i] = s[i];
+    ctr[kC + i] = s[i];
   }
+  // end of king block kb's items
+  auto kb_end = [&](int kb) -> uint32_t { return kb == KB - 1 ? s[(KB - 1) * 33 + 32] + ctr[(KB - 1) * 33 + 32]
+                                                              : s[(kb + 1) * 33]; };
   if (unit_items == 0) {
     // Segment units: unit u of king block kb starts at the first item whose
     // cumulative positions (a bin's items counted at the bin's longest run)
     // reach u * kSegUnitPlies.  Bins are contiguous in item order, so each
     // (kb, bin) thread places the unit starts falling inside its bin.
-    __shared__ uint32_t pb[kItemBins];  // positions before bin i within its king block
-    __shared__ uint32_t ubase[33];      // first unit of each king block
+    __shared__ uint32_t pb[kIB];        // positions before bin i within its king block
+    __shared__ uint32_t ubase[KB + 1];  // first unit of each king block
     for (int k = 0; k < per; ++k) {     // local[k] = count of bin t*per + k
       const int i = t * per + k;
-      if (i < kItemBins) pb[i] = local[k] * seg_bin_longest(i % 33);
+      if (i < kIB) pb[i] = local[k] * seg_bin_longest(i % 33);
     }
     __syncthreads();
-    if (t < 32) {
+    if (t < KB) {
       uint32_t run = 0;
       for (int b = 0; b < 33; ++b) {
         const uint32_t v = pb[t * 33 + b];
@@ -220,20 +229,20 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
       const uint32_t mine = (run + kSegUnitPlies - 1) / kSegUnitPlies;
       uint32_t incl = mine;
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        const uint32_t v = __shfl_up(incl, o, 32);
+      for (int o = 1; o < KB; o <<= 1) {
+        const uint32_t v = __shfl_up(incl, o, KB);
         if (t >= o) incl += v;
       }
       ubase[t] = incl - mine;
-      if (t == 31) {
-        ubase[32] = incl;
-        ctr[kNUnits] = incl;
+      if (t == KB - 1) {
+        ubase[KB] = incl;
+        ctr[kNU] = incl;
       }
     }
     __syncthreads();
     for (int k = 0; k < per; ++k) {
       const int i = t * per + k;
-      if (i >= kItemBins || local[k] == 0) continue;
+      if (i >= kIB || local[k] == 0) continue;
       const int kb = i / 33;
       const uint32_t w = seg_bin_longest(i % 33), p0 = pb[i], p1 = p0 + local[k] * w;
       for (uint32_t u = (p0 + kSegUnitPlies - 1) / kSegUnitPlies; u * kSegUnitPlies < p1; ++u)
@@ -243,27 +252,26 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     // Ends: the next unit's start, or the block's end.  Only .z is written
     // here, so reading a neighbour's .y does not race.  (Unit 0 of a block
     // starts at its first non-empty bin's offset, i.e. the block's first item.)
-    for (uint32_t v = t; v < ubase[32]; v += 1024) {
+    for (uint32_t v = t; v < ubase[KB]; v += 1024) {
       const int kb = units[v].x;
-      const uint32_t kb_end = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
-      units[v].z = v + 1 < ubase[kb + 1] ? units[v + 1].y : (int)kb_end;
+      units[v].z = v + 1 < ubase[kb + 1] ? units[v + 1].y : (int)kb_end(kb);
     }
-  } else if (t < 32) {
+  } else if (t < KB) {
     // Unit table: each king block's item range in chunks of <= unit_items;
     // lane kb counts its block's units, a wave prefix sum places them.
     const int kb = t;
     const uint32_t b = s[kb * 33];
-    const uint32_t e = kb == 31 ? s[31 * 33 + 32] + ctr[kCnt + 31 * 33 + 32] : s[(kb + 1) * 33];
+    const uint32_t e = kb_end(kb);
     const uint32_t mine = (e - b + unit_items - 1) / unit_items;
     uint32_t incl = mine;
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      const uint32_t v = __shfl_up(incl, o, 32);
+    for (int o = 1; o < KB; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, KB);
       if (kb >= o) incl += v;
     }
     uint32_t nu = incl - mine;
     for (uint32_t c = b; c < e; c += unit_items) units[nu++] = make_int4(kb, (int)c, (int)min(e, c + unit_items), 0);
-    if (kb == 31) ctr[kNUnits] = incl;
+    if (kb == KB - 1) ctr[kNU] = incl;
   }
 }
 

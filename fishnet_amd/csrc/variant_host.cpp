@@ -6,7 +6,9 @@
 #include <vector>
 
 #include "board.h"
+#include "builder.h"
 #include "internal.h"
+#include "vboard.h"
 
 using namespace fnnue;
 using namespace fnnue::detail;
@@ -26,16 +28,6 @@ fnnue_vpos pack_v(const VState& v) {
   p.stm = (uint8_t)v.stm;
   std::memcpy(p.hand, v.hand, 10);
   return p;
-}
-
-int piece_of(char c) {
-  const char* w = "PNBRQK";
-  const char* k = "pnbrqk";
-  for (int i = 0; i < 6; ++i) {
-    if (c == w[i]) return i + 1;
-    if (c == k[i]) return i + 9;
-  }
-  return 0;
 }
 
 void start_position(VState& v) {
@@ -126,6 +118,73 @@ void random_step(VState& v, uint64_t& st, int variant) {
   v.stm ^= 1;  // nothing found: pass
 }
 
+// fnnue_vpos of a parsed board, with the evaluator's limits checked on the
+// host: at most 32 pieces on board and in hand, at most 16 of a type in a hand.
+int pack_checked(const vb::VBoard& b, fnnue_vpos* out) {
+  int n = vb::vpopcnt(vb::occupied(b));
+  for (int c = 0; c < 2; ++c)
+    for (int t = 0; t < 5; ++t) {
+      if (b.hand[c][t] > kVHandSlots) return fail(FNNUE_E_FEN, "more than 16 pieces of a type in hand");
+      n += b.hand[c][t];
+    }
+  if (n > 32) return fail(FNNUE_E_FEN, "more than 32 pieces on board and in hand");
+  *out = vb::pack(b);
+  return FNNUE_OK;
+}
+
+std::string square_name(int s) { return std::string{(char)('a' + (s & 7)), (char)('1' + (s >> 3))}; }
+
+// UCI text of a legal move: drops "N@f3", castling king-takes-rook in Chess960
+// positions and the king's two-square step otherwise, promotions "e7e8q".
+std::string vuci(const vb::VBoard& b, const vb::VMove& m) {
+  if (m.kind == 2) return std::string(1, "PNBRQ"[m.piece - 1]) + "@" + square_name(m.to);
+  int to = m.to;
+  if (m.kind == 1 && !b.c960) to = (m.from & 56) + (m.to > m.from ? 6 : 2);
+  std::string u = square_name(m.from) + square_name(to);
+  if (m.kind == 0 && m.piece) u += "nbrq"[m.piece - 2];
+  return u;
+}
+
+bool valid_variant(int variant) { return variant == FNNUE_VARIANT_CRAZYHOUSE || variant == FNNUE_VARIANT_ATOMIC; }
+
+uint64_t vperft(const vb::VBoard& b, int depth) {
+  if (depth == 0) return 1;
+  uint64_t n = 0;
+  vb::for_each_legal(b, [&](const vb::VMove& m) -> bool {
+    if (depth == 1) {
+      ++n;
+    } else {
+      vb::VBoard c = b;
+      vb::do_move(c, m);
+      n += vperft(c, depth - 1);
+    }
+    return true;
+  });
+  return n;
+}
+
+// Replays `moves` from `fen`: f(board) after the root and after every move.
+template <class F>
+int vreplay(int variant, const char* fen, const char* moves, F&& f) {
+  vb::VBoard b;
+  if (!vb::parse_fen(fen, 0, (uint32_t)std::strlen(fen), variant, b))
+    return fail(FNNUE_E_FEN, std::string("unparsable variant FEN: ") + fen);
+  if (int rc = f(b)) return rc;
+  if (!moves) return FNNUE_OK;
+  const uint32_t end = (uint32_t)std::strlen(moves);
+  uint32_t p = 0, st;
+  int len, ply = 0;
+  while ((len = vb::next_token(moves, p, end, st)) > 0) {
+    ++ply;
+    vb::VMove m;
+    if (!vb::match_uci(b, moves + st, len, m))
+      return fail(FNNUE_E_MOVE, "illegal move " + std::string(moves + st, (size_t)len) + " at ply " + std::to_string(ply));
+    vb::do_move(b, m);
+    if (int rc = f(b)) return rc;
+  }
+  return FNNUE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -134,55 +193,11 @@ int fnnue_vpos_from_fen(int variant, const char* fen, fnnue_vpos* out) {
   if (!fen || !out) return fail(FNNUE_E_ARG, "null argument");
   if (variant != FNNUE_VARIANT_CRAZYHOUSE && variant != FNNUE_VARIANT_ATOMIC)
     return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
-  VState v;
-  std::memset(&v, 0, sizeof v);
-  const char* p = fen;
-  int rank = 7, file = 0;
-  bool holdings = false;
-  for (; *p && *p != ' '; ++p) {
-    const char c = *p;
-    if (c == '[') { holdings = true; continue; }
-    if (c == ']') { holdings = false; continue; }
-    if (c == '~') continue;  // promoted-piece mark
-    if (c == '/') {
-      if (--rank < 0) holdings = true;  // a 9th field: holdings
-      file = 0;
-      continue;
-    }
-    if (holdings) {
-      const int pc = piece_of(c);
-      if (!pc || (pc & 7) == 6 || c == '-') {
-        if (c == '-') continue;
-        return fail(FNNUE_E_FEN, std::string("bad holdings piece '") + c + "'");
-      }
-      uint8_t& h = v.hand[5 * (pc >> 3) + (pc & 7) - 1];
-      if (h >= kVHandSlots) return fail(FNNUE_E_FEN, "too many pieces in hand");
-      ++h;
-      continue;
-    }
-    if (c >= '1' && c <= '8') {
-      file += c - '0';
-      continue;
-    }
-    const int pc = piece_of(c);
-    if (!pc || file > 7 || rank < 0) return fail(FNNUE_E_FEN, "bad placement");
-    v.b[rank * 8 + file++] = (uint8_t)pc;
-  }
-  while (*p == ' ') ++p;
-  if (*p != 'w' && *p != 'b') return fail(FNNUE_E_FEN, "missing side to move");
-  v.stm = *p == 'b';
-  int hand_total = 0, n = 0, wk = 0, bk = 0;
-  for (int i = 0; i < 10; ++i) hand_total += v.hand[i];
-  for (int s = 0; s < 64; ++s) {
-    n += v.b[s] != 0;
-    wk += v.b[s] == 6;
-    bk += v.b[s] == 14;
-  }
-  if (wk != 1 || bk != 1) return fail(FNNUE_E_FEN, "needs one king per side");
-  if (hand_total && variant != FNNUE_VARIANT_CRAZYHOUSE) return fail(FNNUE_E_FEN, "holdings in a variant without pockets");
-  if (n + hand_total > 32) return fail(FNNUE_E_FEN, "more than 32 pieces on board and in hand");
-  *out = pack_v(v);
-  return FNNUE_OK;
+  vb::VBoard b;
+  if (!vb::parse_fen(fen, 0, (uint32_t)std::strlen(fen), variant, b))
+    return fail(FNNUE_E_FEN, std::string("unparsable ") + (variant == FNNUE_VARIANT_CRAZYHOUSE ? "crazyhouse" : "atomic") +
+                                 " FEN (placement, holdings, side to move, one king per side): " + fen);
+  return pack_checked(b, out);
 }
 
 int fnnue_random_vpositions(uint64_t seed, int variant, size_t count, uint32_t max_plies, int mode, fnnue_vpos* out,
@@ -216,6 +231,148 @@ int fnnue_random_vpositions(uint64_t seed, int variant, size_t count, uint32_t m
   if (mode == FNNUE_PLAYOUT_PLIES && (!off || off_cap < offs.size())) return fail(FNNUE_E_CAPACITY, "offset buffer too small");
   std::memcpy(out, res.data(), res.size() * sizeof(fnnue_vpos));
   if (mode == FNNUE_PLAYOUT_PLIES) std::memcpy(off, offs.data(), offs.size() * sizeof(uint32_t));
+  return FNNUE_OK;
+}
+
+int fnnue_game_vpositions(int variant, const char* fen, const char* moves, fnnue_vpos* out, size_t cap,
+                          size_t* n_out) {
+  if (!fen || !n_out) return fail(FNNUE_E_ARG, "null argument");
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  std::vector<fnnue_vpos> res;
+  const int rc = vreplay(variant, fen, moves, [&](const vb::VBoard& b) {
+    res.push_back(vb::pack(b));
+    return (int)FNNUE_OK;
+  });
+  if (rc) return rc;
+  *n_out = res.size();
+  if (!out || cap < res.size()) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  std::memcpy(out, res.data(), res.size() * sizeof(fnnue_vpos));
+  return FNNUE_OK;
+}
+
+int fnnue_game_vchildren(int variant, const char* fen, const char* moves, fnnue_vpos* out, size_t cap, uint32_t* off,
+                         size_t off_cap, size_t* n_out, size_t* n_groups) {
+  if (!fen || !n_out || !n_groups) return fail(FNNUE_E_ARG, "null argument");
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  std::vector<fnnue_vpos> res;
+  std::vector<uint32_t> offs{0};
+  const int rc = vreplay(variant, fen, moves, [&](const vb::VBoard& b) {
+    res.push_back(vb::pack(b));
+    vb::for_each_legal(b, [&](const vb::VMove& m) -> bool {
+      vb::VBoard c = b;
+      vb::do_move(c, m);
+      res.push_back(vb::pack(c));
+      return true;
+    });
+    offs.push_back((uint32_t)res.size());
+    return (int)FNNUE_OK;
+  });
+  if (rc) return rc;
+  *n_out = res.size();
+  *n_groups = offs.size() - 1;
+  if (!out || !off || cap < res.size() || off_cap < offs.size()) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  std::memcpy(out, res.data(), res.size() * sizeof(fnnue_vpos));
+  std::memcpy(off, offs.data(), offs.size() * sizeof(uint32_t));
+  return FNNUE_OK;
+}
+
+int fnnue_vperft(int variant, const char* fen, int depth, uint64_t* nodes) {
+  if (!fen || !nodes || depth < 0) return fail(FNNUE_E_ARG, "bad argument");
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  vb::VBoard b;
+  if (!vb::parse_fen(fen, 0, (uint32_t)std::strlen(fen), variant, b)) return fail(FNNUE_E_FEN, "unparsable variant FEN");
+  *nodes = vperft(b, depth);
+  return FNNUE_OK;
+}
+
+int fnnue_random_vgame(uint64_t seed, int variant, const char* fen, uint32_t plies, char* moves, size_t cap,
+                       size_t* len) {
+  if (!fen || !len) return fail(FNNUE_E_ARG, "null argument");
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  vb::VBoard b;
+  if (!vb::parse_fen(fen, 0, (uint32_t)std::strlen(fen), variant, b)) return fail(FNNUE_E_FEN, "unparsable variant FEN");
+  uint64_t st = seed;
+  std::string out;
+  std::vector<vb::VMove> legal;
+  for (uint32_t i = 0; i < plies; ++i) {
+    if (vb::king_sq(b, 0) < 0 || vb::king_sq(b, 1) < 0) break;  // atomic: a king exploded
+    legal.clear();
+    vb::for_each_legal(b, [&](const vb::VMove& m) -> bool {
+      legal.push_back(m);
+      return true;
+    });
+    if (legal.empty()) break;
+    const vb::VMove m = legal[splitmix64(st) % legal.size()];
+    if (!out.empty()) out += ' ';
+    out += vuci(b, m);
+    vb::do_move(b, m);
+  }
+  *len = out.size();
+  if (!moves || cap < out.size() + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  std::memcpy(moves, out.c_str(), out.size() + 1);
+  return FNNUE_OK;
+}
+
+int fnnue_build_vbatch_device(fnnue_ctx* ctx, int variant, const char* d_text, const uint32_t* d_fen_off,
+                              const uint32_t* d_moves_off, size_t ngames, int mode, fnnue_vpos* d_out, size_t cap,
+                              uint32_t* d_off, size_t off_cap, size_t* n_out, size_t* n_groups, void* stream) {
+  if (!ctx || !n_out || !n_groups) return fail(FNNUE_E_ARG, "null argument");
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  if (mode != FNNUE_PLAYOUT_PLIES && mode != FNNUE_PLAYOUT_CHILDREN) return fail(FNNUE_E_ARG, "bad build mode");
+  *n_out = *n_groups = 0;
+  if (ngames == 0) return FNNUE_OK;
+  if (!d_text || !d_fen_off || !d_moves_off) return fail(FNNUE_E_ARG, "null buffer");
+  if (ngames > (1u << 26)) return fail(FNNUE_E_ARG, "too many games");
+  DeviceGuard g(ctx->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const BuildResult R = build_vbatch_device(variant, d_text, d_fen_off, d_moves_off, (uint32_t)ngames,
+                                            mode == FNNUE_PLAYOUT_CHILDREN, d_out, cap, d_off, off_cap, s);
+  if (R.hip != hipSuccess) return hip_fail(R.hip, "device variant batch builder");
+  *n_out = R.n_out;
+  *n_groups = R.n_groups;
+  if (R.err_code == kBuildErrFen) return fail(FNNUE_E_FEN, "unparsable variant FEN in game " + std::to_string(R.err_game));
+  if (R.err_code == kBuildErrMove)
+    return fail(FNNUE_E_MOVE, "illegal move at ply " + std::to_string(R.err_ply) + " of game " +
+                                  std::to_string(R.err_game));
+  if (R.capacity) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  return FNNUE_OK;
+}
+
+int fnnue_build_vbatch(fnnue_ctx* ctx, int variant, const char* text, size_t text_len, const uint32_t* fen_off,
+                       const uint32_t* moves_off, size_t ngames, int mode, fnnue_vpos* out, size_t cap, uint32_t* off,
+                       size_t off_cap, size_t* n_out, size_t* n_groups) {
+  if (!ctx || !n_out || !n_groups || (ngames && (!text || !fen_off || !moves_off)))
+    return fail(FNNUE_E_ARG, "null argument");
+  *n_out = *n_groups = 0;
+  if (ngames == 0) return FNNUE_OK;
+  if (fen_off[ngames] > text_len) return fail(FNNUE_E_ARG, "offsets exceed the text");
+  for (size_t i = 0; i < ngames; ++i)
+    if (fen_off[i] > moves_off[i] || moves_off[i] > fen_off[i + 1]) return fail(FNNUE_E_ARG, "offsets out of order");
+  DeviceGuard g(ctx->device);
+  const size_t text_bytes = (text_len + 255) / 256 * 256;
+  const size_t fo_bytes = (ngames + 1) * 4, mo_bytes = ngames * 4;
+  int rc = ensure_builder_input(ctx, text_bytes + fo_bytes + mo_bytes);
+  if (rc) return rc;
+  char* d_text = ctx->d_btext;
+  uint32_t* d_fo = reinterpret_cast<uint32_t*>(d_text + text_bytes);
+  uint32_t* d_mo = d_fo + (ngames + 1);
+  hipStream_t s = ctx->stream;
+  HIP_TRY(hipMemcpyAsync(d_text, text, text_len, hipMemcpyHostToDevice, s), "H2D");
+  HIP_TRY(hipMemcpyAsync(d_fo, fen_off, fo_bytes, hipMemcpyHostToDevice, s), "H2D");
+  HIP_TRY(hipMemcpyAsync(d_mo, moves_off, mo_bytes, hipMemcpyHostToDevice, s), "H2D");
+  rc = fnnue_build_vbatch_device(ctx, variant, d_text, d_fo, d_mo, ngames, mode, nullptr, 0, nullptr, 0, n_out,
+                                 n_groups, s);
+  if (rc != FNNUE_E_CAPACITY) return rc;  // sizing pass
+  if (!out || !off || cap < *n_out || off_cap < *n_groups + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  if ((rc = ensure_stage(ctx, *n_out, *n_groups + 1))) return rc;
+  fnnue_vpos* d_out = reinterpret_cast<fnnue_vpos*>(ctx->d_pos);  // staging sized for fnnue_vpos
+  uint32_t* d_off = ctx->d_off;
+  rc = fnnue_build_vbatch_device(ctx, variant, d_text, d_fo, d_mo, ngames, mode, d_out, *n_out, d_off, *n_groups + 1,
+                                 n_out, n_groups, s);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, d_out, *n_out * sizeof(fnnue_vpos), hipMemcpyDeviceToHost, s), "D2H");
+  HIP_TRY(hipMemcpyAsync(off, d_off, (*n_groups + 1) * 4, hipMemcpyDeviceToHost, s), "D2H");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
   return FNNUE_OK;
 }
 

@@ -140,6 +140,48 @@ def random_vpositions(seed: int, variant: int, count: int, max_plies: int = 120,
     return out[: n.value], off[: g.value + 1]
 
 
+def game_vpositions(variant: int, fen: str, moves: str | list[str]) -> np.ndarray:
+    """Root + the position after every move of a variant game (host replay)."""
+    if not isinstance(moves, str):
+        moves = " ".join(moves)
+    n = C.c_size_t()
+    cap = moves.count(" ") + 2 if moves.strip() else 1
+    out = N.vpositions_array(cap)
+    N.check(N.lib.fnnue_game_vpositions(variant, fen.encode(), moves.encode(), N.ptr(out), cap, C.byref(n)))
+    return out[: n.value]
+
+
+def game_vchildren(variant: int, fen: str, moves: str | list[str]) -> tuple[np.ndarray, np.ndarray]:
+    """Every ply of a variant game plus its legal children (drops included), STAR groups."""
+    if not isinstance(moves, str):
+        moves = " ".join(moves)
+    nply = (moves.count(" ") + 2) if moves.strip() else 1
+    n, g = C.c_size_t(), C.c_size_t()
+    off = np.zeros(nply + 1, dtype=np.uint32)
+    rc = N.lib.fnnue_game_vchildren(variant, fen.encode(), moves.encode(), None, 0, N.ptr(off), len(off),
+                                    C.byref(n), C.byref(g))
+    if rc != -10:
+        N.check(rc)
+    out = N.vpositions_array(n.value)
+    N.check(N.lib.fnnue_game_vchildren(variant, fen.encode(), moves.encode(), N.ptr(out), len(out), N.ptr(off),
+                                       len(off), C.byref(n), C.byref(g)))
+    return out[: n.value], off[: g.value + 1]
+
+
+def vperft(variant: int, fen: str, depth: int) -> int:
+    nodes = C.c_uint64()
+    N.check(N.lib.fnnue_vperft(variant, fen.encode(), depth, C.byref(nodes)))
+    return nodes.value
+
+
+def random_vgame(seed: int, variant: int, fen: str, plies: int) -> str:
+    """Up to `plies` random legal moves of a variant game as UCI (drops "N@f3")."""
+    n = C.c_size_t()
+    buf = C.create_string_buffer(8 * plies + 16)
+    N.check(N.lib.fnnue_random_vgame(seed, variant, fen.encode(), plies, buf, len(buf), C.byref(n)))
+    return buf.value.decode()
+
+
 def device_count() -> int:
     n = C.c_int()
     N.check(N.lib.fnnue_device_count(C.byref(n)))
@@ -199,6 +241,24 @@ class Evaluator:
         N.check(N.lib.fnnue_eval_vpositions(self._h, N.ptr(vpos), n, N.ptr(psqt), N.ptr(positional)))
         return psqt, positional
 
+    def eval_vgroups(self, vpos: np.ndarray, off: np.ndarray, mode: int = N.GROUP_CHAIN):
+        """Variant positions in CHAIN / STAR groups, accumulators carried along (incremental)."""
+        vpos = np.ascontiguousarray(vpos, dtype=np.uint8).reshape(-1, N.VPOS_BYTES)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        if len(off) < 1 or int(off[-1]) != vpos.shape[0]:
+            raise ValueError("off must have >= 1 entry and end at the number of positions")
+        n = vpos.shape[0]
+        psqt = np.zeros(n, dtype=np.int32)
+        positional = np.zeros(n, dtype=np.int32)
+        N.check(N.lib.fnnue_eval_vgroups(self._h, N.ptr(vpos), n, N.ptr(off), len(off) - 1, mode, N.ptr(psqt),
+                                         N.ptr(positional)))
+        return psqt, positional
+
+    def eval_vgroups_device(self, d_pos: int, d_off: int, ngroups: int, npos: int, mode: int, d_psqt: int,
+                            d_positional: int, stream: int | None):
+        N.check(N.lib.fnnue_eval_vgroups_device(self._h, C.c_void_p(d_pos), C.c_void_p(d_off), ngroups, npos, mode,
+                                                C.c_void_p(d_psqt), C.c_void_p(d_positional), C.c_void_p(stream)))
+
     def eval_vpositions_device(self, d_pos: int, n: int, d_psqt: int, d_positional: int, stream: int | None):
         N.check(N.lib.fnnue_eval_vpositions_device(self._h, C.c_void_p(d_pos), n, C.c_void_p(d_psqt),
                                                    C.c_void_p(d_positional), C.c_void_p(stream)))
@@ -229,6 +289,22 @@ class Evaluator:
         off = np.zeros(g.value + 1, dtype=np.uint32)
         N.check(N.lib.fnnue_build_batch(self._h, text, len(text), N.ptr(fen_off), N.ptr(mv_off), len(games), mode,
                                         N.ptr(out), len(out), N.ptr(off), len(off), C.byref(n), C.byref(g)))
+        return out[: n.value], off[: g.value + 1]
+
+    # Variant games on the device (fnnue_build_vbatch): games = [(fen, "uci ..."), ...].
+    def build_vbatch(self, variant: int, games, mode: int = N.PLAYOUT_PLIES) -> tuple[np.ndarray, np.ndarray]:
+        text, fen_off, mv_off = pack_games(games)
+        n, g = C.c_size_t(), C.c_size_t()
+        rc = N.lib.fnnue_build_vbatch(self._h, variant, text, len(text), N.ptr(fen_off), N.ptr(mv_off), len(games),
+                                      mode, None, 0, None, 0, C.byref(n), C.byref(g))
+        if rc != -10:
+            N.check(rc)
+            return N.vpositions_array(0), np.zeros(1, dtype=np.uint32)
+        out = N.vpositions_array(n.value)
+        off = np.zeros(g.value + 1, dtype=np.uint32)
+        N.check(N.lib.fnnue_build_vbatch(self._h, variant, text, len(text), N.ptr(fen_off), N.ptr(mv_off),
+                                         len(games), mode, N.ptr(out), len(out), N.ptr(off), len(off), C.byref(n),
+                                         C.byref(g)))
         return out[: n.value], off[: g.value + 1]
 
     def perft_device(self, fen: str, depth: int) -> int:

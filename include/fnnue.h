@@ -134,12 +134,52 @@ int fnnue_vpos_from_fen(int variant, const char *fen, fnnue_vpos *out);
  * FNNUE_PLAYOUT_PLIES: every position as CHAIN groups (off[], n_groups + 1). */
 int fnnue_random_vpositions(uint64_t seed, int variant, size_t count, uint32_t max_plies, int mode, fnnue_vpos *out,
                             size_t cap, uint32_t *off, size_t off_cap, size_t *n_out, size_t *n_groups);
+/* Variant games (the expansion of IncomingBatch::from_acquired for the
+ * variants the reference sends to Fairy-Stockfish, [ref] src/queue.rs:524-552,
+ * :530-539): crazyhouse FENs with holdings / promoted marks and UCI moves with
+ * drops ("P@e4"), atomic captures with explosions; every move checked for
+ * legality in its variant (shakmaty's Uci::to_move).  Host replay: the root and
+ * the position after every move (n_moves + 1 records). */
+int fnnue_game_vpositions(int variant, const char *fen, const char *moves, fnnue_vpos *out, size_t cap,
+                          size_t *n_out);
+/* Same plus every legal 1-ply child (drops included) of each position, as STAR
+ * groups (off has n_groups + 1 entries). */
+int fnnue_game_vchildren(int variant, const char *fen, const char *moves, fnnue_vpos *out, size_t cap, uint32_t *off,
+                         size_t off_cap, size_t *n_out, size_t *n_groups);
+/* perft of the variant move generator (known answers pin it). */
+int fnnue_vperft(int variant, const char *fen, int depth, uint64_t *nodes);
+/* Up to `plies` uniformly random legal moves (drops included) from `fen`, as
+ * space-separated UCI; stops when no move is left or a king exploded. */
+int fnnue_random_vgame(uint64_t seed, int variant, const char *fen, uint32_t plies, char *moves, size_t cap,
+                       size_t *len);
+/* The batch expansion on the device, as fnnue_build_batch[_device] (same text
+ * layout, modes FNNUE_PLAYOUT_PLIES / _CHILDREN, sizes reported on
+ * FNNUE_E_CAPACITY), for variant games; records are those of the host replay.
+ * ctx supplies the device and stream (any net). */
+int fnnue_build_vbatch_device(fnnue_ctx *ctx, int variant, const char *d_text, const uint32_t *d_fen_off,
+                              const uint32_t *d_moves_off, size_t ngames, int mode, fnnue_vpos *d_out, size_t cap,
+                              uint32_t *d_off, size_t off_cap, size_t *n_out, size_t *n_groups, void *stream);
+int fnnue_build_vbatch(fnnue_ctx *ctx, int variant, const char *text, size_t text_len, const uint32_t *fen_off,
+                       const uint32_t *moves_off, size_t ngames, int mode, fnnue_vpos *out, size_t cap, uint32_t *off,
+                       size_t off_cap, size_t *n_out, size_t *n_groups);
 /* Evaluation of variant positions on a context created from a variant net
  * (fnnue_ctx_create / fnnue_multi_create): the LDS-stationary feature
  * transformer over the variant tiles, then the MFMA layer stacks. */
 int fnnue_eval_vpositions(fnnue_ctx *ctx, const fnnue_vpos *pos, size_t n, int32_t *psqt, int32_t *positional);
 int fnnue_eval_vpositions_device(fnnue_ctx *ctx, const fnnue_vpos *d_pos, size_t n, int32_t *d_psqt,
                                  int32_t *d_positional, void *stream);
+/* Grouped variant evaluation with accumulator reuse, as fnnue_eval_groups[_device]
+ * (FNNUE_GROUP_CHAIN: a game's plies, e.g. fnnue_build_vbatch's output;
+ * FNNUE_GROUP_STAR: a parent and its children): each accumulator is derived
+ * from the previous ply's / the parent's by the changed board and pocket
+ * features (a crazyhouse capture adds the captured piece's hand row, a drop
+ * removes one), refreshed when the perspective's king moved or more than two
+ * features left or entered (atomic explosions).  Results are identical to
+ * fnnue_eval_vpositions on the same positions. */
+int fnnue_eval_vgroups(fnnue_ctx *ctx, const fnnue_vpos *pos, size_t npos, const uint32_t *off, size_t ngroups,
+                       int mode, int32_t *psqt, int32_t *positional);
+int fnnue_eval_vgroups_device(fnnue_ctx *ctx, const fnnue_vpos *d_pos, const uint32_t *d_off, size_t ngroups,
+                              size_t npos, int mode, int32_t *d_psqt, int32_t *d_positional, void *stream);
 
 /* ---- device context ----
  * Replaces spawning + initialising an engine process ([ref] src/stockfish.rs:

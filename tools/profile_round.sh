@@ -1,6 +1,7 @@
 #!/bin/bash
-# GPU box: rocprofv3 evidence of the current tree for the three bench
-# workloads (config 2 positions, config 3 games, config 4 children):
+# GPU box: rocprofv3 evidence of the current tree for the bench workloads
+# (config 2 positions, config 3 games, config 4 children at its per-GPU scale,
+# config 5 crazyhouse / atomic), each with bench.py's default sizes:
 #   trace/   kernel trace + stats (one run)
 #   pmc_<k>/ one PMC pass per counter set, each its own run (never combined
 #            with tracing domains; every set within the per-block limits)
@@ -20,7 +21,6 @@ SETS=(
 )
 for wl in $WLS; do
   args="--workload $wl"
-  [ "$wl" = children ] && args="$args --games 1000"
   D=$OUT/$wl
   mkdir -p "$D"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- \
