@@ -395,8 +395,11 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
   constexpr bool kLds = W0Lds<HD>::kOn;
   constexpr int kWaves = W0Lds<HD>::kWaves;
   __shared__ v4i w0s[W0Lds<HD>::kWords];
-  __shared__ __attribute__((aligned(16))) uint8_t x1s[kWaves][16][64];
+  // fc_1 inputs: 30 bytes per position, padded to 32 (lanes g >= 2 feed zeros)
+  __shared__ __attribute__((aligned(16))) uint8_t x1s[kWaves][16][32];
   __shared__ int32_t fwds[kWaves][16];
+  // x tile transpose (kLds): 16 rows x 128 B per wave, chunks XOR-swizzled
+  __shared__ v4i xst[kLds ? kWaves : 1][kLds ? 128 : 1];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   if constexpr (kLds) {
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
     }
   }
   // Zero the fc_1 input tile once (k >= 30 stays zero).
-  *reinterpret_cast<v4i*>(&x1s[wv][r16][16 * g]) = (v4i)0;
+  if (g < 2) *reinterpret_cast<v4i*>(&x1s[wv][r16][16 * g]) = (v4i)0;
   if constexpr (kLds) __syncthreads();
   else wave_lds_sync();
   const uint32_t ntiles = (n + 15) / 16;
@@ -440,11 +443,40 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
     for (int b = 0; b < kStacks; ++b)
       if (__ballot(bk == b)) bmask |= 1u << b;
     v4i a[KS];
-    const v4i* xr = reinterpret_cast<const v4i*>(x + (size_t)(row_ok ? prow : p0) * HD);
+    if constexpr (kLds) {
+      // x read as whole 128-B lines: load instruction 2j + h covers rows 8h ..
+      // 8h + 7 of the tile, bytes 128j .. 128j + 127 (lane l: row l / 8, 16-B
+      // chunk l % 8), then each 128-B piece goes through the wave's LDS buffer
+      // into the MFMA A layout (lane l: row l % 16, chunk 4k + l / 16 of K-step
+      // 2j + k).  The MFMA shape itself reads 16 rows x 64 B per instruction,
+      // half lines.  Chunk c of row r sits at c ^ (r & 7): conflict-free writes
+      // (8 lanes = one row) and reads (a ds_read_b128 lane group: 16 distinct
+      // 4-bank sets).
+      constexpr int KP = HD / 128;
+      const int wr = lane >> 3, wc = lane & 7;
+      const uint32_t r0 = p0 + wr, r1 = r0 + 8;
+      const v4i* x0 = reinterpret_cast<const v4i*>(x + (size_t)(r0 < n ? r0 : p0) * HD) + wc;
+      const v4i* x1 = reinterpret_cast<const v4i*>(x + (size_t)(r1 < n ? r1 : p0) * HD) + wc;
 #pragma unroll
-    // x is read exactly once: non-temporal loads (-1 %; non-temporal STORES of x
-    // in the FT cost +3 % there and +6 % here, x then misses the Infinity Cache)
-    for (int s = 0; s < KS; ++s) a[s] = row_ok ? __builtin_nontemporal_load(xr + 4 * s + g) : (v4i)0;
+      // x is read exactly once: non-temporal loads (-1 %; non-temporal STORES of x
+      // in the FT cost +3 % there and +6 % here, x then misses the Infinity Cache)
+      for (int j = 0; j < KP; ++j) {
+        a[2 * j] = r0 < n ? __builtin_nontemporal_load(x0 + 8 * j) : (v4i)0;
+        a[2 * j + 1] = r1 < n ? __builtin_nontemporal_load(x1 + 8 * j) : (v4i)0;
+      }
+      v4i* st = xst[wv];
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {  // in place: LDS ops of one wave complete in order
+        st[wr * 8 + (wc ^ (wr & 7))] = a[2 * j];
+        st[(wr + 8) * 8 + (wc ^ (wr & 7))] = a[2 * j + 1];
+        a[2 * j] = st[r16 * 8 + (g ^ (r16 & 7))];
+        a[2 * j + 1] = st[r16 * 8 + ((4 + g) ^ (r16 & 7))];
+      }
+    } else {
+      const v4i* xr = reinterpret_cast<const v4i*>(x + (size_t)(row_ok ? prow : p0) * HD);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = row_ok ? __builtin_nontemporal_load(xr + 4 * s + g) : (v4i)0;
+    }
     while (bmask) {
       const int b = __builtin_ctz(bmask);
       bmask &= bmask - 1;
