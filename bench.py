@@ -63,8 +63,9 @@ MAIN_KERNEL = {("positions", "sliced"): "ft_slices_kernel", ("positions", "gathe
 def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=1000,
+                    help="timed steps (1000: ~1.5 s of config 2, long enough for an SMI sampler to see the GPU busy)")
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic"], default="positions")
     ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions / variant workloads)")
     ap.add_argument("--games", type=int, default=None,
