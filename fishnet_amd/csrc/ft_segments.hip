@@ -116,7 +116,7 @@ struct VariantFs {
 // Counter layout of a feature set's plan (plan_scan_kernel_t<KB>).
 template <class Fs>
 struct SegCtr {
-  static constexpr int kIB = Fs::KB * 33, kB = kIB + kPosBins, kOff = kB, kCur = 2 * kB;
+  static constexpr int kIB = Fs::KB * 33, kB = kIB + kPosBins, kOff = kB, kCur = 2 * kB, kNUnits = 3 * kB;
   static constexpr size_t kWords = 3 * kB + 16;
 };
 
@@ -645,7 +645,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   // Grid-stride over (unit, slice) pairs: the unit count is known only on the
   // device and its bound (seg_max_units) is far above typical counts.  The
   // grid is a multiple of 8 * S, so every pair keeps its XCD-aware mapping.
-  const uint32_t nunits = ctr[kNUnits];
+  const uint32_t nunits = ctr[SegCtr<Fs>::kNUnits];
   for (uint32_t w = blockIdx.x;; w += gridDim.x) {
     const uint32_t j = w >> 3;
     const uint32_t unit = (j / S) * 8 + (w & 7);

@@ -1,22 +1,22 @@
 #!/bin/bash
-# Builds an experimental variant of libfnnue.so with extra -D flags on every
-# HIP source (the tunables FT_UNIT_ITEMS, SEG_UNIT_PLIES, PLAN_WG, FT_DEPTH;
-# knock-out experiments are patched into a scratch copy, never the shipped
-# sources)
-# into exp/libfnnue_<name>.so (run bench with FNNUE_LIB=...).
-#   usage: tools/exp_build.sh <name> [-DFLAG ...]
+# Builds an experimental variant of libfnnue.so into exp/libfnnue_<name>.so
+# (bench it with FNNUE_LIB=..., tools/exp_run.sh).  The shipped sources are
+# never edited: the csrc tree is copied to build/exp_<name>/, the optional
+# patch (git diff format, paths relative to the repo root) is applied there,
+# extra -D flags (the tunables FT_UNIT_ITEMS, SEG_UNIT_PLIES, PLAN_WG,
+# FT_DEPTH) go to every HIP source.
+#   usage: tools/exp_build.sh <name> [file.patch] [-DFLAG ...]
 set -euo pipefail
-cd "$(dirname "$0")/../fishnet_amd/csrc"
-make -s -j8
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
 name=$1; shift
-mkdir -p ../../exp build/exp
-objs=""
-for src in *.hip; do
-  o=build/exp/${src%.hip}_$name.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c $src -o $o &
-  objs="$objs $o"
-done
-wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../exp/libfnnue_$name.so \
-  build/board.o build/net.o build/capi.o build/multi.o build/variant_host.o build/backend.o $objs -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -lpthread
+patch=""
+if [ $# -gt 0 ] && [ -f "$1" ]; then patch=$(cd "$(dirname "$1")" && pwd)/$(basename "$1"); shift; fi
+W=$ROOT/build/exp_$name
+rm -rf "$W"; mkdir -p "$W/fishnet_amd" "$ROOT/exp"
+cp -r "$ROOT/fishnet_amd/csrc" "$W/fishnet_amd/csrc"
+cp -r "$ROOT/include" "$W/include"
+rm -rf "$W/fishnet_amd/csrc/build"
+if [ -n "$patch" ]; then (cd "$W" && patch -p1 --quiet < "$patch"); fi
+make -s -C "$W/fishnet_amd/csrc" -j8 ARCH=gfx950 HIPFLAGS="--offload-arch=gfx950 --offload-compress $*" >/dev/null
+cp "$W/fishnet_amd/libfnnue.so" "$ROOT/exp/libfnnue_$name.so"
 echo "exp/libfnnue_$name.so"
