@@ -27,6 +27,9 @@ Other workloads (the other BASELINE configs, measured for DESIGN.md):
   --workload crazyhouse / atomic
                        config 5: Fairy-Stockfish HalfKAv2-variants nets (synthetic), 1M random-walk
                        variant positions per GPU (pockets / explosions), from scratch
+  --workload crazyhouse-games / atomic-games
+                       config 5 along games: every ply of 10k random legal variant games per GPU
+                       (drops, pockets, explosions), incremental CHAIN (fnnue_eval_vgroups_device)
 
 roofline: the binding resource of the dominant kernel (ft_slices for config
 2, ft_segments for configs 3/4) from the committed PMC profile of this tree
@@ -66,7 +69,8 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=1000,
                     help="timed steps (1000: ~1.5 s of config 2, long enough for an SMI sampler to see the GPU busy)")
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic"], default="positions")
+    ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic", "crazyhouse-games",
+                                           "atomic-games"], default="positions")
     ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions / variant workloads)")
     ap.add_argument("--games", type=int, default=None,
                     help="games per GPU (games: 10,000 = config 3; children: 5,000 ~ 12.5M positions per GPU = "
@@ -202,13 +206,15 @@ def stdout_to_stderr():
 
 
 def variant_of(F, workload):
-    return {"crazyhouse": F.VARIANT_CRAZYHOUSE, "atomic": F.VARIANT_ATOMIC}.get(workload)
+    return {"crazyhouse": F.VARIANT_CRAZYHOUSE, "atomic": F.VARIANT_ATOMIC}.get(workload.replace("-games", ""))
 
 
 def make_inputs(F, args, seed, threads):
     off = None
     variant = variant_of(F, args.workload)
-    if variant is not None:
+    if variant is not None and args.workload.endswith("-games"):
+        pos, off = F.random_vgames(seed + 1, variant, args.games, 160, threads=threads)
+    elif variant is not None:
         pos = F.random_vpositions(seed, variant, args.positions, 160)
     elif args.workload == "positions":
         pos = F.random_playouts(seed, args.positions, 0, 160, threads=threads)
@@ -252,8 +258,9 @@ def main():
     variant = variant_of(F, args.workload)
     if variant is not None and args.small_net:
         raise SystemExit("--small-net applies to the chess workloads")
-    groups = args.workload in ("games", "children")
-    gmode = None if not groups else (F.GROUP_CHAIN if args.workload == "games" else F.GROUP_STAR)
+    vgames = args.workload.endswith("-games")
+    groups = args.workload in ("games", "children") or vgames
+    gmode = None if not groups else (F.GROUP_STAR if args.workload == "children" else F.GROUP_CHAIN)
 
     # ---- net: rank 0 / device 0 holds it, RCCL broadcasts it over xGMI ----
     t0 = time.time()
@@ -303,7 +310,22 @@ def main():
         shards.append(Shard(torch, torch.device("cuda", d), pos, off, args.small_net))
     pos, off = host0
     board = boards_of(pos)
-    if variant is not None:
+    if variant is not None and vgames:
+        hand = pos[:, 33:43].astype(np.int64)
+        starts = off[:-1].astype(np.int64)
+        has_base = np.ones(len(pos), dtype=bool)
+        has_base[starts] = False
+        base_idx = np.arange(len(pos)) - 1
+        base_idx[~has_base] = 0
+        # board rows as for chess, plus each pocket change as a hand row, both perspectives
+        rows = rows_incremental(board, board[base_idx], has_base) + np.where(
+            has_base, 2 * np.abs(hand - hand[base_idx]).sum(axis=1), 2 * hand.sum(axis=1))
+        vname = args.workload.replace("-games", "")
+        workload = ("BASELINE config 5 along games: every ply of %d random legal %s games per GPU (L~U[0,160], %s), "
+                    "incremental CHAIN accumulators, synthetic Fairy-Stockfish HalfKAv2-variants net (HD=%d)"
+                    % (args.games, vname, "drops, captures to the pocket" if vname == "crazyhouse" else "explosions",
+                       args.hd))
+    elif variant is not None:
         hand = pos[:, 33:43].astype(np.int64).sum(axis=1)
         rows = rows_scratch(board) + 2 * hand
         workload = ("BASELINE config 5: %s random-walk positions (pseudo-legal moves, %s; L~U[0,160]), "
@@ -335,7 +357,15 @@ def main():
 
     def run_net(k):
         outs = [(s.psqt, s.positional) if k == 0 else (s.small[0], s.small[1]) for s in shards]
-        if variant is not None and launch == "devices":
+        if variant is not None and vgames and launch == "devices":
+            multi.eval_vgroups_device([s.pos.data_ptr() for s in shards], [s.off.data_ptr() for s in shards],
+                                      [s.ng for s in shards], [s.n for s in shards], gmode,
+                                      [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs], streams)
+        elif variant is not None and vgames:
+            s, e = shards[0], evs[k][0]
+            e.eval_vgroups_device(s.pos.data_ptr(), s.off.data_ptr(), s.ng, s.n, gmode, outs[0][0].data_ptr(),
+                                  outs[0][1].data_ptr(), torch.cuda.current_stream().cuda_stream)
+        elif variant is not None and launch == "devices":
             multi.eval_vpositions_device([s.pos.data_ptr() for s in shards], [s.n for s in shards],
                                          [o[0].data_ptr() for o in outs], [o[1].data_ptr() for o in outs],
                                          streams)
@@ -485,7 +515,9 @@ def main():
                "cpu": {k: cpus[k] for k in ("model", "os_cpu_count", "affinity", "cgroup_quota", "omp_num_threads")},
                "sample": f"{done} positions of the same workload (from-scratch refresh per position; {cpu_el:.1f} s "
                          f"wall on {threads} threads; oracle/variant_oracle.c = scalar C restatement of "
-                         f"Fairy-Stockfish's HalfKAv2-variants NNUE, -O3, no SIMD: Fairy-Stockfish itself is absent)"}
+                         f"Fairy-Stockfish's HalfKAv2-variants NNUE, -O3, no SIMD: Fairy-Stockfish itself is absent"
+                         + ("; the GPU line is incremental along the games, the CPU port refreshes every ply"
+                            if vgames else "") + ")"}
         parity = {"checked": min(done, npos), "mismatches": mism}
     elif rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import OracleNet  # cpu_baseline leg: oracle/nnue_cpu_simd.c is the timed CPU port
@@ -550,7 +582,12 @@ def main():
         target = multi if launch == "devices" else evs[0][0]
         t0 = time.perf_counter()
         for _ in range(reps):
-            if variant is not None:
+            if variant is not None and vgames:
+                if launch == "devices":
+                    hp, hq = evs[0][0].eval_vgroups(pos, off, gmode)  # device 0's shard
+                else:
+                    hp, hq = target.eval_vgroups(hpos, hoff, gmode)
+            elif variant is not None:
                 hp, hq = target.eval_vpositions(hpos)  # fnnue_multi_eval_vpositions for the devices launch
             else:
                 hp, hq = target.eval_positions(hpos) if not groups else target.eval_groups(hpos, hoff, gmode)

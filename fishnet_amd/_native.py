@@ -107,6 +107,8 @@ SIGNATURES = {
     "fnnue_multi_sync": ([_vp], _i32),
     "fnnue_multi_eval_vpositions": ([_vp, _vp, _sz, _vp, _vp], _i32),
     "fnnue_multi_eval_vpositions_device": ([_vp, _P(_vp), _P(_sz), _P(_vp), _P(_vp), _P(_vp)], _i32),
+    "fnnue_multi_eval_vgroups_device": ([_vp, _P(_vp), _P(_vp), _P(_sz), _P(_sz), _i32, _P(_vp), _P(_vp), _P(_vp)],
+                                        _i32),
     "fnnue_partition_groups": ([_vp, _sz, _i32, _vp], _i32),
     "fnnue_net_load_variant": ([C.c_char_p, _i32, _P(_vp)], _i32),
     "fnnue_net_load_variant_mem": ([_vp, _sz, _i32, _P(_vp)], _i32),
@@ -118,6 +120,7 @@ SIGNATURES = {
     "fnnue_game_vchildren": ([_i32, C.c_char_p, C.c_char_p, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_vperft": ([_i32, C.c_char_p, _i32, _P(_u64)], _i32),
     "fnnue_random_vgame": ([_u64, _i32, C.c_char_p, _u32, C.c_char_p, _sz, _P(_sz)], _i32),
+    "fnnue_random_vgames": ([_u64, _i32, _sz, _u32, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_build_vbatch_device": ([_vp, _i32, _vp, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz), _vp],
                                   _i32),
     "fnnue_build_vbatch": ([_vp, _i32, C.c_char_p, _sz, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)],

@@ -228,6 +228,18 @@ int fnnue_multi_eval_groups_device(fnnue_multi* m, const fnnue_pos* const* d_pos
   return FNNUE_OK;
 }
 
+int fnnue_multi_eval_vgroups_device(fnnue_multi* m, const fnnue_vpos* const* d_pos, const uint32_t* const* d_off,
+                                    const size_t* ngroups, const size_t* npos, int mode, int32_t* const* d_psqt,
+                                    int32_t* const* d_positional, void* const* streams) {
+  if (!m || !d_pos || !d_off || !ngroups || !npos || !d_psqt || !d_positional)
+    return fail(FNNUE_E_ARG, "null argument");
+  for (size_t i = 0; i < m->ctx.size(); ++i)
+    if (int rc = fnnue_eval_vgroups_device(m->ctx[i], d_pos[i], d_off[i], ngroups[i], npos[i], mode, d_psqt[i],
+                                           d_positional[i], stream_of(streams, i)))
+      return fail(rc, "device " + std::to_string(m->devices[i]) + ": " + fnnue_last_error());
+  return FNNUE_OK;
+}
+
 int fnnue_multi_eval_vpositions(fnnue_multi* m, const fnnue_vpos* pos, size_t n, int32_t* psqt, int32_t* positional) {
   if (!m) return fail(FNNUE_E_ARG, "null multi");
   if (n == 0) return FNNUE_OK;

@@ -2,6 +2,7 @@
 // crazyhouse holdings -> fnnue_vpos, and seeded random walks that produce
 // variant positions for tests and the bench (include/fnnue.h).
 #include <cstring>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -310,6 +311,78 @@ int fnnue_random_vgame(uint64_t seed, int variant, const char* fen, uint32_t pli
   *len = out.size();
   if (!moves || cap < out.size() + 1) return fail(FNNUE_E_CAPACITY, "output buffer too small");
   std::memcpy(moves, out.c_str(), out.size() + 1);
+  return FNNUE_OK;
+}
+
+int fnnue_random_vgames(uint64_t seed, int variant, size_t count, uint32_t max_plies, int threads, fnnue_vpos* out,
+                        size_t cap, uint32_t* off, size_t off_cap, size_t* n_out, size_t* n_groups) {
+  if (!n_out || !n_groups) return fail(FNNUE_E_ARG, "null argument");
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  const char* start = variant == FNNUE_VARIANT_CRAZYHOUSE ? "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR[] w KQkq - 0 1"
+                                                          : "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1";
+  vb::VBoard root;
+  vb::parse_fen(start, 0, (uint32_t)std::strlen(start), variant, root);
+  // Game i: L ~ U[0, max_plies] uniformly random legal moves from (seed, i),
+  // stopping when no move is left or a king exploded (that last position is
+  // dropped: it has no king to evaluate).  Independent of the thread count.
+  struct Part {
+    std::vector<fnnue_vpos> pos;
+    std::vector<uint32_t> sizes;
+  };
+  std::vector<Part> parts(threads);
+  auto work = [&](int t) {
+    const size_t b = count * t / threads, e = count * (t + 1) / threads;
+    Part& P = parts[t];
+    std::vector<vb::VMove> legal;
+    for (size_t i = b; i < e; ++i) {
+      uint64_t st = seed ^ (0xD1B54A32D192ED03ull * (i + 1));
+      const uint32_t L = (uint32_t)(splitmix64(st) % ((uint64_t)max_plies + 1));
+      vb::VBoard v = root;
+      const size_t before = P.pos.size();
+      P.pos.push_back(vb::pack(v));
+      for (uint32_t k = 0; k < L; ++k) {
+        legal.clear();
+        vb::for_each_legal(v, [&](const vb::VMove& m) -> bool {
+          legal.push_back(m);
+          return true;
+        });
+        if (legal.empty()) break;
+        vb::do_move(v, legal[splitmix64(st) % legal.size()]);
+        if (vb::king_sq(v, 0) < 0 || vb::king_sq(v, 1) < 0) break;
+        P.pos.push_back(vb::pack(v));
+      }
+      P.sizes.push_back((uint32_t)(P.pos.size() - before));
+    }
+  };
+  try {
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  } catch (const std::exception& ex) {
+    return fail(FNNUE_E_OOM, std::string("variant game generation failed: ") + ex.what());
+  }
+  size_t total = 0, groups = 0;
+  for (auto& P : parts) {
+    total += P.pos.size();
+    groups += P.sizes.size();
+  }
+  *n_out = total;
+  *n_groups = groups;
+  if (!out || cap < total) return fail(FNNUE_E_CAPACITY, "output buffer too small");
+  if (!off || off_cap < groups + 1) return fail(FNNUE_E_CAPACITY, "offset buffer too small");
+  size_t k = 0, gk = 0;
+  off[0] = 0;
+  for (auto& P : parts) {
+    std::memcpy(out + k, P.pos.data(), P.pos.size() * sizeof(fnnue_vpos));
+    for (uint32_t sz : P.sizes) {
+      off[gk + 1] = off[gk] + sz;
+      ++gk;
+    }
+    k += P.pos.size();
+  }
   return FNNUE_OK;
 }
 

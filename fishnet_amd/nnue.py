@@ -182,6 +182,17 @@ def random_vgame(seed: int, variant: int, fen: str, plies: int) -> str:
     return buf.value.decode()
 
 
+def random_vgames(seed: int, variant: int, count: int, max_plies: int = 160, threads: int = 8):
+    """Every ply of seeded random legal variant games, CHAIN groups -> (positions, offsets)."""
+    cap = count * (max_plies + 1)
+    out = N.vpositions_array(cap)
+    off = np.zeros(count + 1, dtype=np.uint32)
+    n, g = C.c_size_t(), C.c_size_t()
+    N.check(N.lib.fnnue_random_vgames(seed, variant, count, max_plies, threads, N.ptr(out), cap, N.ptr(off), len(off),
+                                      C.byref(n), C.byref(g)))
+    return out[: n.value], off[: g.value + 1]
+
+
 def device_count() -> int:
     n = C.c_int()
     N.check(N.lib.fnnue_device_count(C.byref(n)))
@@ -431,6 +442,11 @@ class MultiEvaluator:
     def eval_vpositions_device(self, d_pos, n, d_psqt, d_positional, streams=None) -> None:
         N.check(N.lib.fnnue_multi_eval_vpositions_device(self._h, _ptrs(d_pos), _sizes(n), _ptrs(d_psqt),
                                                          _ptrs(d_positional), _streams(streams)))
+
+    def eval_vgroups_device(self, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional, streams=None) -> None:
+        N.check(N.lib.fnnue_multi_eval_vgroups_device(self._h, _ptrs(d_pos), _ptrs(d_off), _sizes(ngroups),
+                                                      _sizes(npos), mode, _ptrs(d_psqt), _ptrs(d_positional),
+                                                      _streams(streams)))
 
     def eval_groups_device(self, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional, streams=None) -> None:
         N.check(N.lib.fnnue_multi_eval_groups_device(self._h, _ptrs(d_pos), _ptrs(d_off), _sizes(ngroups),

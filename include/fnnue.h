@@ -152,6 +152,12 @@ int fnnue_vperft(int variant, const char *fen, int depth, uint64_t *nodes);
  * space-separated UCI; stops when no move is left or a king exploded. */
 int fnnue_random_vgame(uint64_t seed, int variant, const char *fen, uint32_t plies, char *moves, size_t cap,
                        size_t *len);
+/* Test / bench inputs: every ply of `count` seeded random LEGAL games of the
+ * variant from its start position (L ~ U[0, max_plies] plies, drops included),
+ * as CHAIN groups; a game ends early with no legal move or an exploded king
+ * (that position is not emitted).  Deterministic for (seed, index). */
+int fnnue_random_vgames(uint64_t seed, int variant, size_t count, uint32_t max_plies, int threads, fnnue_vpos *out,
+                        size_t cap, uint32_t *off, size_t off_cap, size_t *n_out, size_t *n_groups);
 /* The batch expansion on the device, as fnnue_build_batch[_device] (same text
  * layout, modes FNNUE_PLAYOUT_PLIES / _CHILDREN, sizes reported on
  * FNNUE_E_CAPACITY), for variant games; records are those of the host replay.
@@ -233,6 +239,11 @@ int fnnue_multi_sync(fnnue_multi *m);
 int fnnue_multi_eval_vpositions(fnnue_multi *m, const fnnue_vpos *pos, size_t n, int32_t *psqt, int32_t *positional);
 int fnnue_multi_eval_vpositions_device(fnnue_multi *m, const fnnue_vpos *const *d_pos, const size_t *n,
                                        int32_t *const *d_psqt, int32_t *const *d_positional, void *const *streams);
+/* Grouped variant positions on every device (fnnue_eval_vgroups_device per
+ * device, one shard of whole games each), as fnnue_multi_eval_groups_device. */
+int fnnue_multi_eval_vgroups_device(fnnue_multi *m, const fnnue_vpos *const *d_pos, const uint32_t *const *d_off,
+                                    const size_t *ngroups, const size_t *npos, int mode, int32_t *const *d_psqt,
+                                    int32_t *const *d_positional, void *const *streams);
 /* Splits groups off[0..ngroups] into nparts contiguous runs of whole groups
  * with about equal position counts: part k = groups [cut[k], cut[k+1]),
  * cut has nparts + 1 entries.  Host only. */

@@ -197,3 +197,22 @@ def test_variant_builder_entry_points_without_gpu():
     assert e.value.name == "FNNUE_E_FEN"
     assert N.lib.fnnue_build_vbatch(None, ZH, b"", 0, None, None, 0, N.PLAYOUT_PLIES, None, 0, None, 0,
                                     None, None) == -1
+
+
+@pytest.mark.parametrize("variant", [ZH, AT])
+def test_random_vgames_deterministic_and_replayable(variant):
+    """fnnue_random_vgames (bench / test inputs): every ply of legal random games
+    as CHAIN groups, independent of the thread count; each game's first
+    position is the start position, every position has both kings."""
+    a, oa = nnue.random_vgames(9, variant, 300, 120, threads=1)
+    b, ob = nnue.random_vgames(9, variant, 300, 120, threads=7)
+    assert np.array_equal(a, b) and np.array_equal(oa, ob)
+    assert len(oa) == 301 and oa[0] == 0 and oa[-1] == len(a) and np.all(np.diff(oa.astype(np.int64)) >= 1)
+    start = nnue.game_vpositions(variant, ZH_START if variant == ZH else START, "")[0]
+    assert all(np.array_equal(a[o], start) for o in oa[:-1])
+    bd = np.zeros((len(a), 64), np.uint8)
+    bd[:, 0::2] = a[:, :32] & 15
+    bd[:, 1::2] = a[:, :32] >> 4
+    assert np.all((bd == 6).sum(1) == 1) and np.all((bd == 14).sum(1) == 1)
+    if variant == ZH:
+        assert int(a[:, 33:43].sum()) > 0  # pockets fill up

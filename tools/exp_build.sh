@@ -13,10 +13,11 @@ patch=""
 if [ $# -gt 0 ] && [ -f "$1" ]; then patch=$(cd "$(dirname "$1")" && pwd)/$(basename "$1"); shift; fi
 W=$ROOT/build/exp_$name
 rm -rf "$W"; mkdir -p "$W/fishnet_amd" "$ROOT/exp"
-cp -r "$ROOT/fishnet_amd/csrc" "$W/fishnet_amd/csrc"
-cp -r "$ROOT/include" "$W/include"
-rm -rf "$W/fishnet_amd/csrc/build"
-if [ -n "$patch" ]; then (cd "$W" && patch -p1 --quiet < "$patch"); fi
+make -s -C "$ROOT/fishnet_amd/csrc" -j8 ARCH=gfx950 >/dev/null
+# timestamps kept: make rebuilds only what the patch touches (and what includes it)
+cp -a "$ROOT/fishnet_amd/csrc" "$W/fishnet_amd/csrc"
+cp -a "$ROOT/include" "$W/include"
+if [ -n "$patch" ]; then sleep 1; (cd "$W" && patch -p1 --quiet < "$patch"); fi
 make -s -C "$W/fishnet_amd/csrc" -j8 ARCH=gfx950 HIPFLAGS="--offload-arch=gfx950 --offload-compress $*" >/dev/null
 cp "$W/fishnet_amd/libfnnue.so" "$ROOT/exp/libfnnue_$name.so"
 echo "exp/libfnnue_$name.so"

@@ -15,7 +15,7 @@ for st in $STEPS; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
         || { echo "smoke rc=$?"; tail -20 $O/smoke.log; exit 1; }
       tail -1 $O/smoke.log ;;
-    positions|games|children|crazyhouse|atomic|devices)
+    positions|games|children|crazyhouse|atomic|crazyhouse-games|atomic-games|devices)
       a="--workload $st"; [ $st = devices ] && a="--launch devices --gpus 1"
       timeout -k 10 400 python bench.py $a $BENCH_ARGS > $O/bench_$st.json 2> $O/bench_$st.err \
         || { echo "bench $st rc=$?"; tail -20 $O/bench_$st.err; exit 1; }

@@ -9,7 +9,7 @@
 #   usage: tools/profile_round.sh <tag> [workload ...]   (default: all three)
 set -uo pipefail
 TAG=${1:-rXX}; shift || true
-WLS=${*:-positions games children crazyhouse atomic}
+WLS=${*:-positions games children crazyhouse atomic crazyhouse-games atomic-games}
 OUT=$PWD/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
