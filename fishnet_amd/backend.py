@@ -37,7 +37,7 @@ class _Acquired(C.Structure):
 
 class _Response(C.Structure):
     _fields_ = [("position_id", C.c_uint32), ("skipped", C.c_uint8), ("score_kind", C.c_uint8),
-                ("depth", C.c_uint8), ("pad", C.c_uint8), ("score", C.c_int64), ("psqt", C.c_int32),
+                ("depth", C.c_uint8), ("matrix", C.c_uint8), ("score", C.c_int64), ("psqt", C.c_int32),
                 ("positional", C.c_int32), ("nodes", C.c_uint64), ("time_ms", C.c_uint64), ("nps", C.c_uint32),
                 ("best_move", C.c_char * 8)]
 
@@ -72,6 +72,7 @@ class PositionResponse:
     nps: int = 0
     best_move: str | None = None
     skipped: bool = False
+    matrix: bool = False              # AnalysisPart::Matrix (the batch asked for multipv)
 
 
 @dataclass
@@ -155,7 +156,8 @@ class GpuEvalStub:
                     continue
                 rows.append(PositionResponse(
                     r.position_id, Score("mate" if r.score_kind == SCORE_MATE else "cp", int(r.score)), r.psqt,
-                    r.positional, r.depth, r.nodes, r.time_ms, r.nps, r.best_move.decode() or None))
+                    r.positional, r.depth, r.nodes, r.time_ms, r.nps, r.best_move.decode() or None,
+                    matrix=bool(r.matrix)))
             res.append(rows)
         return res
 
@@ -184,8 +186,8 @@ def into_analysis(responses: Sequence[PositionResponse]) -> str:
             arr[i] = _Response(r.position_id, 1)
             continue
         kind = SCORE_MATE if r.score.kind == "mate" else SCORE_CP
-        arr[i] = _Response(r.position_id, 0, kind, r.depth, 0, r.score.value, r.psqt, r.positional, r.nodes,
-                           r.time_ms, r.nps, (r.best_move or "").encode())
+        arr[i] = _Response(r.position_id, 0, kind, r.depth, 1 if r.matrix else 0, r.score.value, r.psqt,
+                           r.positional, r.nodes, r.time_ms, r.nps, (r.best_move or "").encode())
     n = C.c_size_t()
     N.lib.fnnue_backend_analysis_json(arr, len(responses), None, 0, C.byref(n))
     buf = C.create_string_buffer(n.value + 1)

@@ -330,7 +330,7 @@ void fnnue_backend::run(Job& j) {
   for (size_t i = 0; i < nb; ++i) {
     const fnnue_acquired& a = j.batches[i];
     if (j.rc[i]) continue;
-    if (!chess_variant(a.variant) || a.multipv > 1) {  // Fairy-Stockfish / MultiPV search: not this backend
+    if (!chess_variant(a.variant) || a.multipv < 0) {  // Fairy-Stockfish (routed by flavour): not this backend
       j.rc[i] = FNNUE_E_ARG;
       continue;
     }
@@ -382,6 +382,7 @@ void fnnue_backend::run(Job& j) {
         continue;
       }
       const size_t x = base[i] + r.position_id;
+      r.matrix = j.batches[i].multipv > 0 ? 1 : 0;  // Work::matrix_wanted: multipv is Some
       r.psqt = hpsqt[x];
       r.positional = hpositional[x];
       r.score_kind = FNNUE_SCORE_CP;
@@ -488,10 +489,18 @@ int fnnue_backend_analysis_json(const fnnue_position_response* r, size_t n, char
       s += "{\"skipped\":true}";
       continue;
     }
-    // AnalysisPart::Best: pv omitted when empty, nps omitted when None
-    std::snprintf(tmp, sizeof(tmp), "{\"score\":{\"%s\":%lld},\"depth\":%u,\"nodes\":%llu,\"time\":%llu",
-                  r[i].score_kind == FNNUE_SCORE_MATE ? "mate" : "cp", (long long)r[i].score, (unsigned)r[i].depth,
-                  (unsigned long long)r[i].nodes, (unsigned long long)r[i].time_ms);
+    // AnalysisPart::Best: pv omitted when empty, nps omitted when None.
+    // AnalysisPart::Matrix: pv / score matrices [multipv - 1][depth]; static
+    // eval fills multipv 1 at depth 0 with an empty pv.
+    const char* kind = r[i].score_kind == FNNUE_SCORE_MATE ? "mate" : "cp";
+    if (r[i].matrix)
+      std::snprintf(tmp, sizeof(tmp), "{\"pv\":[[[]]],\"score\":[[{\"%s\":%lld}]],\"depth\":%u,\"nodes\":%llu,"
+                    "\"time\":%llu", kind, (long long)r[i].score, (unsigned)r[i].depth, (unsigned long long)r[i].nodes,
+                    (unsigned long long)r[i].time_ms);
+    else
+      std::snprintf(tmp, sizeof(tmp), "{\"score\":{\"%s\":%lld},\"depth\":%u,\"nodes\":%llu,\"time\":%llu", kind,
+                    (long long)r[i].score, (unsigned)r[i].depth, (unsigned long long)r[i].nodes,
+                    (unsigned long long)r[i].time_ms);
     s += tmp;
     if (r[i].nps) {
       std::snprintf(tmp, sizeof(tmp), ",\"nps\":%u", r[i].nps);

@@ -65,7 +65,9 @@ typedef struct {
 typedef struct {
   const char *batch_id;            /* Work::id (BatchId), copied into logs / errors */
   int work;                        /* FNNUE_WORK_* */
-  int multipv;                     /* Work::Analysis multipv; 0 or 1 (static eval has one line) */
+  int multipv;                     /* Work::Analysis multipv: 0 = None; >= 1 = Some(k): the response is the
+                                      matrix form (AnalysisPart::Matrix, Work::matrix_wanted, api.rs:179-187)
+                                      with its one line (static eval has no second PV) at depth 0 */
   const char *position;            /* root FEN (X-FEN / Shredder castling accepted) */
   const char *variant;             /* "standard", "chess960", "fromPosition", NULL / "" = standard */
   const char *moves;               /* space-separated UCI (Chess960 king-takes-rook accepted) */
@@ -79,7 +81,7 @@ typedef struct {
   uint8_t skipped;       /* 1: Skip::Skip (AnalysisPart::Skipped) */
   uint8_t score_kind;    /* FNNUE_SCORE_* */
   uint8_t depth;
-  uint8_t pad;
+  uint8_t matrix;        /* 1: serialise as AnalysisPart::Matrix (multipv requested) */
   int64_t score;         /* centipawns (side to move) */
   int32_t psqt;          /* the raw NNUE terms the score came from */
   int32_t positional;
@@ -110,7 +112,9 @@ int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nba
 /* The `analysis` array fishnet submits for one analysis batch
  * (CompletedBatch::into_analysis, queue.rs:715-727; AnalysisPart / Score
  * serialisation, api.rs:355-388): {"skipped":true} or {"score":{"cp":..},
- * "depth":..,"nodes":..,"time":..,"nps":..} per position, as JSON.  Writes
+ * "depth":..,"nodes":..,"time":..,"nps":..} per position, or for a MultiPV
+ * batch the matrix form {"pv":[[[]]],"score":[[{"cp":..}]],"depth":0,...}
+ * (Matrix::set(multipv 1, depth 0): one row, one column), as JSON.  Writes
  * at most cap bytes including the NUL; *len = the full length (without NUL);
  * FNNUE_E_CAPACITY when it did not fit. */
 int fnnue_backend_analysis_json(const fnnue_position_response *r, size_t n, char *buf, size_t cap, size_t *len);

@@ -41,6 +41,17 @@ def test_analysis_json_shapes():
     assert B.into_analysis([]) == "[]"
 
 
+def test_analysis_json_matrix_form():
+    """A MultiPV batch (Work::matrix_wanted, [ref] src/api.rs:179-187) is
+    answered as AnalysisPart::Matrix: pv / score matrices indexed [multipv -
+    1][depth] (Matrix::set, src/ipc.rs:77-86); static evaluation fills line 1
+    at depth 0 with an empty pv."""
+    rs = [B.PositionResponse(0, B.Score("cp", 41), depth=0, nodes=1, time_ms=3, nps=9, matrix=True),
+          B.PositionResponse(1, None, skipped=True)]
+    s = B.into_analysis(rs)
+    assert s == '[{"pv":[[[]]],"score":[[{"cp":41}]],"depth":0,"nodes":1,"time":3,"nps":9},{"skipped":true}]'
+
+
 def test_analysis_json_capacity():
     import ctypes as C
     arr = (B._Response * 1)()

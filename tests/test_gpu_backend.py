@@ -75,7 +75,13 @@ def test_failed_batches_are_isolated(chan):
     res = stub.go(bodies)
     codes = {b.batch_id: (r.code if isinstance(r, B.PositionFailed) else 0) for b, r in zip(bodies, res)}
     assert codes["badmove"] == -8 and codes["badfen"] == -9
-    assert codes["zh"] == -1 and codes["mpv"] == -1
+    assert codes["zh"] == -1 and codes["mpv"] == 0  # MultiPV: answered in the matrix form (one line)
+    mpv = res[4]
+    assert len(mpv) == 2 and all(r.matrix for r in mpv)
+    ps, po = expect(on, START, "e2e4")
+    assert [r.psqt for r in mpv] == ps.tolist() and [r.positional for r in mpv] == po.tolist()
+    m = json.loads(B.into_analysis(mpv))
+    assert m[0]["pv"] == [[[]]] and m[0]["score"] == [[{"cp": mpv[0].score.value}]] and m[0]["depth"] == 0
     assert codes["threekings"] != 0
     assert codes["good"] == 0 and codes["good2"] == 0
     for i in (1, 6):
