@@ -681,7 +681,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
     for (int k = 0; k < kTileLoads; ++k)
       if ((int)threadIdx.x + 1024 * k < kTileU4) {
         uint4 v = t[k];
-        if constexpr (kSwar) v = make_uint4(swar_word(v.x), swar_word(v.y), swar_word(v.z), swar_word(v.w));
+        if constexpr (kSwar) v = swar_tile_words(v);
         img[threadIdx.x + 1024 * k] = v;
       }
     if (s == 0) {
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
       if constexpr (kSwar) {
         b_lo = swar_words(b_lo);
-        b_hi = swar_words(b_hi);
+        b_hi = swar_words_hi(b_hi);
       }
       accum_row<kSwar>(kv, b_lo, b_hi);
       if constexpr (kSwar) {  // both halves of every word offset by 0x8000 (transform4_swar)

@@ -171,7 +171,7 @@ __device__ __forceinline__ void slice_pass(const PassFetch& f, uint2* __restrict
 // lists are fetched two passes ahead while the current pass reads the LDS tile.
 // Items of a unit are sorted by piece count, so a pass's longest list is that
 // of its item 7 (clamped into the unit).  kSwar: the tile is converted to SWAR
-// words on its way into LDS and rows are summed as 32-bit words (swar_word).
+// words on its way into LDS and rows are summed as 32-bit words (swar_tile_words).
 template <int HD, bool kSwar, class G = ChessGeom>
 __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict__ tiles,
                                                          const int16_t* __restrict__ ftb,
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
   for (int k = 0; k < kTileLoads; ++k)
     if ((int)threadIdx.x + 1024 * k < kTileU4) {
       uint4 v = t[k];
-      if constexpr (kSwar) v = make_uint4(swar_word(v.x), swar_word(v.y), swar_word(v.z), swar_word(v.w));
+      if constexpr (kSwar) v = swar_tile_words(v);
       img[threadIdx.x + 1024 * k] = v;
     }
   if (s == 0) {
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(1024) void ft_slices_kernel(const uint4* __restrict
     const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
     if constexpr (kSwar) {
       b_lo = swar_words(b_lo);
-      b_hi = swar_words(b_hi);
+      b_hi = swar_words_hi(b_hi);
     }
     accum_row<kSwar>(kv, b_lo, b_hi);
     if constexpr (kSwar) {  // both halves of every word offset by 0x8000 (transform4_swar)

@@ -277,9 +277,15 @@ void pack_image(const Net& net, uint8_t* dst) {
 int32_t accumulator_bound(const int16_t* ft_w, const int16_t* ft_bias, uint32_t hd, int variant) {
   const int kRows = (int)(variant == kVariantChess ? kFeatures / 32 : variant_rows(variant));  // rows per king block
   const int kBlocks = variant == kVariantChess ? 32 : 64;
-  const uint32_t ncol = hd / 2;          // even columns
+  // Columns a SWAR word's exactness depends on: the first half's even columns
+  // (low halves, partial sums must stay in int16) and every second-half column,
+  // counted twice (kept doubled in the tile, swar_word_hi in sliced_common.h).
+  std::vector<uint32_t> cols;
+  for (uint32_t c = 0; c < hd / 2; c += 2) cols.push_back(c);
+  for (uint32_t c = hd / 2; c < hd; ++c) cols.push_back(c);
+  const size_t ncol = cols.size();
   int64_t worst = 0;
-  std::vector<int32_t> mag((size_t)ncol * kRows);  // [even column][row], |w|
+  std::vector<int32_t> mag(ncol * kRows);  // [column][row], |w|
   for (int kb = 0; kb < kBlocks; ++kb) {
     // own-king row of king block kb: plane 10, oriented king square on files e-h
     // (KingBuckets is a bijection kb <-> oriented square; upstream half_ka_v2_hm.h);
@@ -287,14 +293,14 @@ int32_t accumulator_bound(const int16_t* ft_w, const int16_t* ft_bias, uint32_t 
     const int krow = variant == kVariantChess ? 640 + 8 * (7 - (kb >> 2)) + (7 - (kb & 3)) : 640 + kb;
     const int16_t* blk = ft_w + (size_t)kb * kRows * hd;
     for (int r = 0; r < kRows; ++r)
-      for (uint32_t c = 0; c < ncol; ++c)
-        mag[(size_t)c * kRows + r] = r == krow ? 0 : std::abs((int32_t)blk[(size_t)r * hd + 2 * c]);
-    for (uint32_t c = 0; c < ncol; ++c) {
-      int32_t* m = mag.data() + (size_t)c * kRows;
+      for (size_t i = 0; i < ncol; ++i)
+        mag[i * kRows + r] = r == krow ? 0 : std::abs((int32_t)blk[(size_t)r * hd + cols[i]]);
+    for (size_t i = 0; i < ncol; ++i) {
+      int32_t* m = mag.data() + i * kRows;
       std::nth_element(m, m + 31, m + kRows, std::greater<int32_t>());
-      int64_t b = std::abs((int32_t)ft_bias[2 * c] + (int32_t)blk[(size_t)krow * hd + 2 * c]);
+      int64_t b = std::abs((int32_t)ft_bias[cols[i]] + (int32_t)blk[(size_t)krow * hd + cols[i]]);
       for (int k = 0; k < 31; ++k) b += m[k];
-      worst = std::max(worst, b);
+      worst = std::max(worst, cols[i] < hd / 2 ? b : 2 * b);
     }
   }
   return (int32_t)std::min<int64_t>(worst, INT32_MAX);

@@ -77,11 +77,13 @@ struct ImageLayout {
 ImageLayout image_layout(uint32_t hd, uint32_t nfeat = kFeatures);
 void pack_image(const Net& net, uint8_t* dst);  // dst has image_layout(hd).total bytes
 
-// Largest possible |true int32 sum| of an even ("low") accumulator column over
-// every reachable accumulator: per king block kb and even column j,
+// Largest possible |true int32 sum| of an accumulator column over every
+// reachable accumulator: per king block kb and column j,
 // |bias_j + w[own king row][j]| + the 31 largest |w[r][j]| of the other rows
-// of kb (a position has at most 31 pieces besides the perspective's king).
-// Below 2^15 the feature transformer may sum column pairs as 32-bit words
+// of kb (a position has at most 31 pieces besides the perspective's king),
+// taken over the first half's even ("low") columns and, counted twice, over
+// every second-half column (those are kept doubled in the SWAR tile).  Below
+// 2^15 the feature transformer may sum column pairs as 32-bit words
 // (ft_slices' SWAR rows) and still be bit-exact.
 // rows / blocks: the feature set's rows per own-king block and block count
 // (chess: 704 x 32, own king row 640 + KingBuckets order; variants: rows x 64,

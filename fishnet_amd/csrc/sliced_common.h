@@ -461,13 +461,29 @@ __device__ __forceinline__ u16x4 swar_words(u16x4 v) {
 // restoring the borrow a negative l took from the high half) and h + 0x8000
 // in its high half, both mod 2^16.  A saturating u16 subtract of 0x8000 is
 // max(column, 0) on both halves at once, so no unpacking is needed.
+//
+// The second half's columns (the `hi` words, columns HD/2..HD-1) are kept
+// DOUBLED in the tile and the bias (swar_word_hi): hi - 0x8000 saturated is
+// max(2 col, 0), its min with 254 is 2 clamp(col, 0, 127), and a * that is
+// already (a b) << 1, whose high byte is SF's (a b) >> 7 — one shift per pair
+// fewer.  Exact while every reachable second-half column stays below 2^14 in
+// magnitude (accumulator_bound counts it twice, net.cpp).
 constexpr uint32_t kSwarOffset = 0x80008000u;
+__device__ __forceinline__ uint32_t swar_word_hi(uint32_t packed) {
+  return swar_word((packed << 1) & 0xFFFEFFFEu);
+}
+__device__ __forceinline__ u16x4 swar_words_hi(u16x4 v) {
+  const u32x2 w = __builtin_bit_cast(u32x2, v);
+  return __builtin_bit_cast(u16x4, u32x2{swar_word_hi(w.x), swar_word_hi(w.y)});
+}
+__device__ __forceinline__ uint4 swar_tile_words(uint4 v) {  // 16 B of a tile row: 4 lo columns, 4 hi columns
+  return make_uint4(swar_word(v.x), swar_word(v.y), swar_word_hi(v.z), swar_word_hi(v.w));
+}
 __device__ __forceinline__ uint32_t transform4_swar(u16x4 lo, u16x4 hi) {
-  const u16x4 off = (u16x4)0x8000, top = (u16x4)127;
+  const u16x4 off = (u16x4)0x8000, top = (u16x4)127, top2 = (u16x4)254;
   const u16x4 a = __builtin_elementwise_min(__builtin_elementwise_sub_sat(lo, off), top);
-  const u16x4 b = __builtin_elementwise_min(__builtin_elementwise_sub_sat(hi, off), top);
-  const u16x4 pr = (a * b) << (u16x4)1;
-  const u32x2 w = __builtin_bit_cast(u32x2, pr);
+  const u16x4 b2 = __builtin_elementwise_min(__builtin_elementwise_sub_sat(hi, off), top2);
+  const u32x2 w = __builtin_bit_cast(u32x2, a * b2);
   return __builtin_amdgcn_perm(w.y, w.x, 0x07050301u);
 }
 

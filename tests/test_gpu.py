@@ -510,6 +510,60 @@ def test_swar_rows_match_packed_rows(ev_cache, seed, hd, flags):
     assert e.value.name == "FNNUE_E_ARCH"
 
 
+def edge_net(seed: int, hd: int, mag: tuple[int, int]) -> bytes:
+    """A synthetic net whose FT columns each keep one sign over every row with
+    |w| in [mag[0], mag[1]] and a zero bias: full-board accumulators reach
+    31-32 times mag, close to the doubled-column SWAR limit (2^14).  The first
+    half's odd columns stay small (|w| <= 12) so that half the transform pairs
+    do not saturate and the evaluation still depends on the position."""
+    data = bytearray(net_bytes(seed, hd, 0))
+    desc_len = int(np.frombuffer(data, np.uint32, 1, 8)[0])
+    o = 12 + desc_len + 4
+    rng = np.random.default_rng(seed)
+    sign = np.where(rng.random(hd) < 0.5, -1, 1)
+    w = rng.integers(mag[0], mag[1] + 1, size=(22528, hd)) * sign
+    small = np.arange(hd)[1:hd // 2:2]
+    w[:, small] = rng.integers(-12, 13, size=(22528, small.size))
+    data[o:o + 2 * hd] = bytes(2 * hd)
+    data[o + 2 * hd:o + 2 * hd + 2 * 22528 * hd] = w.astype(np.int16).tobytes()
+    return bytes(data)
+
+
+def test_swar_exact_at_the_doubled_column_limit():
+    """Second-half columns are summed doubled: a net whose
+    accumulators come within ~15 % of 2^14 still runs SWAR rows and stays
+    bit-exact against packed rows and the oracle (a wrap would turn a
+    saturated 127 into 0); a net just past the limit falls back to packed
+    rows."""
+    data = edge_net(21, 256, (400, 500))
+    net = F.Net.from_bytes(data)
+    assert 31 * 400 * 2 < net.accumulator_bound() < 32768
+    ev, on = F.Evaluator(net, 0), OracleNet(data)
+    try:
+        assert ev.swar()[0]
+        pos = F.random_playouts(21, 20000, 0, 40, threads=8)  # early plies: 28-32 pieces
+        a = ev.eval_positions(pos)
+        ev.set_swar(False)
+        b = ev.eval_positions(pos)
+        ev.set_swar(True)
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+        ops, opo, rc = on.eval_packed(pos, threads=8)
+        assert rc == 0 and np.array_equal(a[0], ops) and np.array_equal(a[1], opo)
+        gpos, off = F.random_playouts(22, 200, 0, 60, mode=N.PLAYOUT_PLIES, threads=8)
+        gs, go = ev.eval_groups(gpos, off, N.GROUP_CHAIN)
+        ops, opo, rc = on.eval_packed(gpos, threads=8)
+        assert rc == 0 and np.array_equal(gs, ops) and np.array_equal(go, opo)
+    finally:
+        ev.close()
+    over = F.Net.from_bytes(edge_net(21, 256, (520, 540)))
+    assert over.accumulator_bound() >= 32768
+    evo = F.Evaluator(over, 0)
+    try:
+        assert evo.swar()[0] is False
+    finally:
+        evo.close()
+
+
 @pytest.mark.skipif(not os.environ.get("FNNUE_NET"), reason="set FNNUE_NET=<path to a real .nnue> to run")
 def test_real_net_file_matches_oracle():
     """Opt-in: a real Stockfish net (e.g. nn-ad9b42354671.nnue, [ref] build.rs:7)

@@ -240,7 +240,8 @@ def test_device_entry_points_fail_cleanly_without_gpu():
 
 def test_accumulator_bound_decides_swar():
     """SWAR row sums (ft_slices) are exact only if no reachable accumulator's
-    even column leaves int16 range: realistic synthetic nets qualify, the
+    low column leaves int16 range and no doubled second-half column leaves it
+    (net.h): realistic synthetic nets qualify, the
     int16-wrap stress net does not (the library then keeps packed adds)."""
     import fishnet_amd as F
     b = F.Net.from_bytes(F.synthesize_net(1, 1024, 0)).accumulator_bound()

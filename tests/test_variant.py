@@ -123,21 +123,25 @@ def test_random_vpositions_are_valid():
 
 
 def numpy_accumulator_bound(data: bytes, hd: int, rows: int, blocks: int, king_row) -> int:
-    """The SWAR bound restated over the raw file: per king block and even
-    column, |bias + own-king row| + the 31 largest |w| of the other rows."""
+    """The SWAR bound restated over the raw file: per king block and column,
+    |bias + own-king row| + the 31 largest |w| of the other rows, over the
+    first half's even columns and, doubled, every second-half column."""
     desc_len = int(np.frombuffer(data, np.uint32, 1, 8)[0])
     o = 12 + desc_len + 4  # header, then the FT hash
-    bias = np.frombuffer(data, np.int16, hd, o).astype(np.int64)
-    w = np.frombuffer(data, np.int16, blocks * rows * hd, o + 2 * hd).reshape(blocks, rows, hd)[:, :, 0::2]
+    cols = np.concatenate([np.arange(0, hd // 2, 2), np.arange(hd // 2, hd)])
+    scale = np.where(cols < hd // 2, 1, 2)
+    bias = np.frombuffer(data, np.int16, hd, o).astype(np.int64)[cols]
+    w = np.frombuffer(data, np.int16, blocks * rows * hd, o + 2 * hd).reshape(blocks, rows, hd)[:, :, cols]
     w = np.abs(w.astype(np.int64))
     worst = 0
     for kb in range(blocks):
         kr = king_row(kb)
         m = w[kb].copy()
-        base = np.abs(bias[0::2] + np.frombuffer(data, np.int16, hd, o + 2 * hd + 2 * (kb * rows + kr) * hd)[0::2])
+        krow = np.frombuffer(data, np.int16, hd, o + 2 * hd + 2 * (kb * rows + kr) * hd).astype(np.int64)[cols]
+        base = np.abs(bias + krow)
         m[kr] = 0
         top = -np.sort(-m, axis=0)[:31].sum(axis=0)
-        worst = max(worst, int((base + top).max()))
+        worst = max(worst, int(((base + top) * scale).max()))
     return worst
 
 
