@@ -117,7 +117,7 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant) {
   const size_t tiles = variant == kVariantChess ? sliced_tiles_bytes(hd) : variant_tiles_bytes(hd, variant);
   const size_t units = std::max({sliced_max_units(chunk), seg_max_units(chunk), variant_max_units(chunk)});
   if (hipMalloc(&P.tiles, tiles) != hipSuccess ||
-      hipMalloc(&P.ctr, std::max(sliced_ctr_words(), variant_ctr_words()) * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&P.ctr, std::max({sliced_ctr_words(), variant_ctr_words(), seg_ctr_words()}) * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&P.units, units * 16) != hipSuccess ||
       hipMalloc(&P.items, (size_t)2 * chunk * sizeof(uint32_t)) != hipSuccess ||
       hipMalloc(&P.flist, (size_t)2 * chunk * 32 * sizeof(uint16_t)) != hipSuccess ||

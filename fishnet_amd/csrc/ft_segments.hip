@@ -29,10 +29,10 @@
 //                 block counts in seg_delta, seg_scan_blocks, then local
 //                 scans in seg_items_scan, which also maps item k -> its
 //                 root position
-//   seg_place     segment length per refresh (next refresh / group parent);
-//                 delta records placed at root + rank (a segment's plies
-//                 contiguous)
-//   seg_count / plan_scan / seg_scatter   counting sort of items by
+//   seg_place     segment length per refresh (next refresh / group parent)
+//                 and the item histogram; delta records placed at root +
+//                 rank (a segment's plies contiguous)
+//   plan_scan / seg_scatter   counting sort of items by
 //                 (king block, length bin), unit table cut every
 //                 kSegUnitPlies (16384) positions of work per king block,
 //                 full lists (write_rows)
@@ -48,6 +48,7 @@
 // refresh.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "variant_common.h"
@@ -67,6 +68,7 @@ struct ChessFs {
   using Pos = fnnue_pos;
   using G = ChessGeom;
   static constexpr int KB = 32;
+  static constexpr int kClasses = 4;  // list-length classes per length bin (seg_count_class)
   static constexpr bool kHand = false;
   static constexpr uint32_t kNone = 16u * G::kRows;
   struct Dec {
@@ -75,20 +77,37 @@ struct ChessFs {
     int nfeat;
     bool ok;
   };
+  template <bool kOcc = true>
   __device__ static __forceinline__ Dec decode(const Pos* p) {
     Dec d;
-    d.b = lane_decode(p);
+    d.b = lane_decode<kOcc>(p);
     d.nfeat = d.b.cnt;
     d.ok = d.b.ok;
     return d;
   }
-  __device__ static __forceinline__ int block(int c, int ksq) { return king_block(c, ksq); }
-  __device__ static __forceinline__ uint32_t board_entry(int c, int s, int pc, int ksq, int kb) {
-    return 16u * (uint32_t)(make_index(c, s, pc, ksq) - kRowsPerBlock * kb);
+  // The base of a delta: its board words, with validity and king squares
+  // from an earlier decode (seg_info).
+  __device__ static __forceinline__ Dec load_base(const Pos* p, uint32_t info) {
+    Dec d;
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d.b.w[k] = pw[k];
+    d.ok = (info & 1u) != 0;
+    d.b.wk = (int)((info >> 1) & 63u);
+    d.b.bk = (int)((info >> 7) & 63u);
+    return d;
   }
-  __device__ static __forceinline__ void write_list(const Dec& d, int c, uint32_t it, const uint32_t* ctr,
-                                                    uint32_t* mine, uint16_t* flist) {
-    write_rows(d.b, c, c ? d.b.bk : d.b.wk, it, ctr, mine, flist);
+  __device__ static __forceinline__ int block(int c, int ksq) { return king_block(c, ksq); }
+  // 16 * (make_index(c, s, pc, ksq) - 704 * kb): the oriented square plus
+  // 64 * the plane (nibble table), the king block cancels
+  __device__ static __forceinline__ uint32_t board_entry(int c, int s, int pc, int ksq, int) {
+    const uint32_t flip = (c ? 56u : 0u) ^ ((ksq & 7) < 4 ? 7u : 0u);
+    const uint64_t ptab = c ? plane_table(1) : plane_table(0);
+    return 16u * (((uint32_t)s ^ flip) + 64u * (uint32_t)((ptab >> (4 * pc)) & 15u));
+  }
+  __device__ static __forceinline__ void write_list(const Dec& d, int c, uint32_t it, uint32_t pp, uint32_t* mine,
+                                                    uint16_t* flist) {
+    write_rows(d.b, c, c ? d.b.bk : d.b.wk, it, pp, mine, flist);
   }
 };
 
@@ -99,24 +118,39 @@ struct VariantFs {
   using G = VariantGeom<R>;
   static constexpr int KB = 64;
   static constexpr bool kHand = V == kVariantCrazyhouse;
+  static constexpr int kClasses = kHand ? 1 : 4;
   static constexpr uint32_t kNone = 16u * R;
   using Dec = VariantBoard;
-  __device__ static __forceinline__ Dec decode(const Pos* p) { return vdecode(p, kHand); }
+  template <bool kOcc = true>
+  __device__ static __forceinline__ Dec decode(const Pos* p) { return vdecode<kOcc>(p, kHand); }
+  __device__ static __forceinline__ Dec load_base(const Pos* p, uint32_t info) {
+    Dec d;
+    const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d.b.w[k] = pw[k];
+    const uint8_t* h = reinterpret_cast<const uint8_t*>(p) + 33;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) d.hand[j] = h[j];
+    d.ok = (info & 1u) != 0;
+    d.b.wk = (int)((info >> 1) & 63u);
+    d.b.bk = (int)((info >> 7) & 63u);
+    return d;
+  }
   __device__ static __forceinline__ int block(int c, int ksq) { return vblock(c, ksq); }
   __device__ static __forceinline__ uint32_t board_entry(int c, int s, int pc, int, int) {
     return 16u * vboard_row(c, s, pc);
   }
-  __device__ static __forceinline__ void write_list(const Dec& d, int c, uint32_t it, const uint32_t* ctr,
-                                                    uint32_t* mine, uint16_t* flist) {
-    const int kb = vblock(c, c ? d.b.bk : d.b.wk);
-    vwrite_rows<R>(d, c, it, (it - ctr[kVOff + kb * 33]) & 1u, mine, flist);
+  __device__ static __forceinline__ void write_list(const Dec& d, int c, uint32_t it, uint32_t pp, uint32_t* mine,
+                                                    uint16_t* flist) {
+    vwrite_rows<R>(d, c, it, pp, mine, flist);
   }
 };
 
 // Counter layout of a feature set's plan (plan_scan_kernel_t<KB>).
 template <class Fs>
 struct SegCtr {
-  static constexpr int kIB = Fs::KB * 33, kB = kIB + kPosBins, kOff = kB, kCur = 2 * kB, kNUnits = 3 * kB;
+  static constexpr int kNB = 33 * Fs::kClasses;  // bins per king block
+  static constexpr int kIB = Fs::KB * kNB, kB = kIB + kPosBins, kOff = kB, kCur = 2 * kB, kNUnits = 3 * kB;
   static constexpr size_t kWords = 3 * kB + 16;
 };
 
@@ -156,15 +190,27 @@ __device__ __forceinline__ uint2 group_range(const uint2* __restrict__ span, uin
   return make_uint2(min(a, i), min(max(b, i + 1), n));
 }
 
-// Refresh flags r0 / r1 and delta records of position i (both perspectives).
+// Validity and king squares of a decoded position, for the next position's
+// delta (seg_delta_kernel shares them through LDS).
+template <class Dec>
+__device__ __forceinline__ uint32_t seg_info(const Dec& d) {
+  return (d.ok ? 1u : 0u) | (uint32_t)d.b.wk << 1 | (uint32_t)d.b.bk << 7;
+}
+
+// Refresh flags r0 / r1 and delta records of position i (both perspectives),
+// B = its decode.  The base's validity and king squares come from `info`
+// (the block's positions i0 .. i0 + 255) when it lies in this block: the
+// base of a CHAIN ply is the previous position, so only a wave's first lane
+// decodes a second board (a wave with any such lane pays the whole decode).
 template <class Fs>
 __device__ __forceinline__ void seg_delta_one(const typename Fs::Pos* __restrict__ pos, uint32_t n,
                                               const uint2* __restrict__ span, uint32_t sbase, int star,
                                               uint32_t* __restrict__ ref,
                                               uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
-                                              uint32_t* __restrict__ err, uint32_t i, uint32_t& r0, uint32_t& r1) {
+                                              uint32_t* __restrict__ err, uint32_t i, uint32_t i0,
+                                              const uint32_t* info, const typename Fs::Dec& B, uint32_t& r0,
+                                              uint32_t& r1) {
   using Dec = typename Fs::Dec;
-  const Dec B = Fs::decode(pos + i);
   if (!B.ok) {
     // no item, no accumulator; counted as a refresh so that STAR ranks skip it
     bucket[i] = 0xFF;
@@ -179,63 +225,93 @@ __device__ __forceinline__ void seg_delta_one(const typename Fs::Pos* __restrict
   const bool has_base = i > first;
   Dec A;
   bool base_ok = false;
-  uint64_t changed = 0;
+  const uint32_t bi = star ? first : i - 1;  // the base, when has_base
   if (has_base) {
-    A = Fs::decode(pos + (star ? first : i - 1));
+    const uint32_t ai = bi >= i0 ? info[bi - i0] : seg_info(Fs::template decode<false>(pos + bi));
+    A = Fs::load_base(pos + bi, ai);
     base_ok = A.ok;
+  }
+  // Changed squares as a 64-bit mask, then at most four of them, one uniform
+  // step each (a loop per board word ran a step for every word in which any
+  // lane of the wave had a change: eight steps for a wave's moves).  The
+  // nibbles are read back as bytes of the two records, both just loaded (a
+  // register array indexed by a lane-varying square would live in scratch).
+  uint64_t ch = 0;
+  if (has_base) {
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      changed |= (uint64_t)nibble_bits(~zero_nibbles(A.b.w[k] ^ B.b.w[k]) & 0x88888888u) << (8 * k);
+      ch |= (uint64_t)nibble_bits(~zero_nibbles(A.b.w[k] ^ B.b.w[k]) & 0x88888888u) << (8 * k);
   }
+  const int nch = __popcll(ch);
+  // Removed / added entries of both perspectives in named slots (a register
+  // array indexed by the running count would live in scratch as well); the
+  // counts are the same for both perspectives.
+  const int ks0 = B.b.wk, ks1 = B.b.bk;
+  const int kb0 = Fs::block(0, ks0), kb1 = Fs::block(1, ks1);
+  uint32_t r00 = Fs::kNone, r01 = Fs::kNone, r10 = Fs::kNone, r11 = Fs::kNone;
+  uint32_t a00 = Fs::kNone, a01 = Fs::kNone, a10 = Fs::kNone, a11 = Fs::kNone;
+  auto put = [](uint32_t& x0, uint32_t& x1, int cnt, uint32_t e) {
+    x0 = cnt == 0 ? e : x0;
+    x1 = cnt == 1 ? e : x1;
+  };
+  int nr = 0, na = 0;
+  if (base_ok && nch <= 4) {
+    const uint8_t* pa = reinterpret_cast<const uint8_t*>(pos + bi);
+    const uint8_t* pb = reinterpret_cast<const uint8_t*>(pos + i);
+    for (uint64_t m = ch; m; m &= m - 1) {
+      const int s = __builtin_ctzll(m), sh = 4 * (s & 1);
+      const int was = (pa[s >> 1] >> sh) & 15, now = (pb[s >> 1] >> sh) & 15;
+      if (was) {
+        put(r00, r01, nr, Fs::board_entry(0, s, was, ks0, kb0));
+        put(r10, r11, nr, Fs::board_entry(1, s, was, ks1, kb1));
+        ++nr;
+      }
+      if (now) {
+        put(a00, a01, na, Fs::board_entry(0, s, now, ks0, kb0));
+        put(a10, a11, na, Fs::board_entry(1, s, now, ks1, kb1));
+        ++na;
+      }
+    }
+    if constexpr (Fs::kHand) {
+      // pocket slot j holding `was` pieces before and `now` after: the rows
+      // of its pieces was .. now - 1 are added, now .. was - 1 removed
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int ksq = c ? B.b.bk : B.b.wk;
-    bool refresh = !base_ok || (c ? A.b.bk : A.b.wk) != ksq || __popcll(changed) > 4;
-    uint32_t rem[2] = {Fs::kNone, Fs::kNone}, add[2] = {Fs::kNone, Fs::kNone};
-    if (!refresh) {
-      const int kb = Fs::block(c, ksq);
-      int nr = 0, na = 0;
-      for (uint64_t m = changed; m; m &= m - 1) {
-        const int s = __builtin_ctzll(m);
-        const int was = nibble_at(A.b.w, s), now = nibble_at(B.b.w, s);
-        if (was) {
-          if (nr < 2) rem[nr] = Fs::board_entry(c, s, was, ksq, kb);
+      for (int j = 0; j < 10; ++j) {
+        const uint32_t was = A.hand[j], now = B.hand[j];
+        for (uint32_t k = now; k < was && nr <= 2; ++k) {
+          put(r00, r01, nr, 16u * vhand_row(0, j, k));
+          put(r10, r11, nr, 16u * vhand_row(1, j, k));
           ++nr;
         }
-        if (now) {
-          if (na < 2) add[na] = Fs::board_entry(c, s, now, ksq, kb);
+        for (uint32_t k = was; k < now && na <= 2; ++k) {
+          put(a00, a01, na, 16u * vhand_row(0, j, k));
+          put(a10, a11, na, 16u * vhand_row(1, j, k));
           ++na;
         }
       }
-      if constexpr (Fs::kHand) {
-        // pocket slot j holding `was` pieces before and `now` after: the rows
-        // of its pieces was .. now - 1 are added, now .. was - 1 removed
-#pragma unroll
-        for (int j = 0; j < 10; ++j) {
-          const uint32_t was = A.hand[j], now = B.hand[j];
-          for (uint32_t k = now; k < was && nr <= 2; ++k) {
-            if (nr < 2) rem[nr] = 16u * vhand_row(c, j, k);
-            ++nr;
-          }
-          for (uint32_t k = was; k < now && na <= 2; ++k) {
-            if (na < 2) add[na] = 16u * vhand_row(c, j, k);
-            ++na;
-          }
-        }
-      }
-      refresh = nr > 2 || na > 2;  // never for a legal chess move; explosions / arbitrary groups refresh
     }
-    ref[c * n + i] = refresh ? 1u : 0u;
+  }
+  // refresh: own king moved, invalid base, > 4 changed squares, or more than
+  // two removed / added rows (never for a legal chess move; explosions and
+  // arbitrary groups refresh)
+  const bool common = !base_ok || nch > 4 || nr > 2 || na > 2;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const bool refresh = common || (c ? A.b.bk != ks1 : A.b.wk != ks0);
+    // a refresh carries its king block and count class for the item
+    // histogram (seg_place)
+    ref[c * n + i] = refresh ? 1u | (uint32_t)(c ? kb1 : kb0) << 8 | seg_count_class<Fs::kClasses>((uint32_t)B.nfeat) << 16 : 0u;
     (c ? r1 : r0) = refresh ? 1u : 0u;
     if (!refresh) {
       const uint32_t half = B.b.stm == c ? 0u : 1u;
-      dtmp[c * n + i] = make_uint4((2u * i + half) | bk << 25, rem[0] | rem[1] << 16, add[0] | add[1] << 16, 0u);
+      const uint32_t rm = c ? r10 | r11 << 16 : r00 | r01 << 16, ad = c ? a10 | a11 << 16 : a00 | a01 << 16;
+      dtmp[c * n + i] = make_uint4((2u * i + half) | bk << 25, rm, ad, 0u);
     }
   }
 }
 
 // The first kernel of a chunk's plan: block 0 also zeroes the counter block
-// (read by seg_count / plan_scan / seg_scatter) instead of a memset launch.
+// (read by seg_place / plan_scan / seg_scatter) instead of a memset launch.
 template <class Fs>
 __global__ __launch_bounds__(256) void seg_delta_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
                                                         const uint2* __restrict__ span, uint32_t sbase, int star,
@@ -243,11 +319,18 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const typename Fs::Pos* 
                                                         uint4* __restrict__ dtmp, uint8_t* __restrict__ bucket,
                                                         uint32_t* __restrict__ err, uint32_t* __restrict__ bsum,
                                                         uint32_t* __restrict__ ctr, uint32_t ctr_words) {
+  __shared__ uint32_t info[256];
   if (blockIdx.x == 0)
     for (uint32_t k = threadIdx.x; k < ctr_words; k += blockDim.x) ctr[k] = 0;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+  typename Fs::Dec B;
+  B.ok = false;
+  B.b.wk = B.b.bk = 0;
+  if (i < n) B = Fs::template decode<false>(pos + i);
+  info[threadIdx.x] = seg_info(B);
+  __syncthreads();
   uint32_t r0 = 0, r1 = 0;
-  if (i < n) seg_delta_one<Fs>(pos, n, span, sbase, star, ref, dtmp, bucket, err, i, r0, r1);
+  if (i < n) seg_delta_one<Fs>(pos, n, span, sbase, star, ref, dtmp, bucket, err, i, i0, info, B, r0, r1);
   // refresh counts of this block's 256 positions, per perspective (seg_scan_blocks)
   const int c0 = __syncthreads_count((int)r0), c1 = __syncthreads_count((int)r1);
   if (threadIdx.x == 0) {
@@ -262,26 +345,30 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const typename Fs::Pos* 
 constexpr uint32_t kMaxScanBlocks = 8192;
 __global__ __launch_bounds__(1024) void seg_scan_blocks_kernel(uint32_t* __restrict__ bsum, uint32_t nb, uint32_t n,
                                                                uint32_t* __restrict__ cref) {
-  __shared__ uint32_t part[1024];
+  __shared__ uint32_t part[16];
   const uint32_t m = 2 * nb, per = (m + 1023) / 1024, t = threadIdx.x;
   uint32_t sum = 0;
   for (uint32_t k = 0; k < per; ++k) sum += t * per + k < m ? bsum[t * per + k] : 0u;
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    const uint32_t v = t >= o ? part[t - o] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  // per-thread sums scanned inside each wave by shuffles, then over the 16
+  // wave totals
+  const uint32_t lane = t & 63, wv = t >> 6;
+  uint32_t incl = sum;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+    if (lane >= o) incl += v;
   }
-  uint32_t run = part[t] - sum;
+  if (lane == 63) part[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (uint32_t w = 0; w < wv; ++w) run += part[w];
   for (uint32_t k = 0; k < per; ++k)
     if (t * per + k < m) {
       const uint32_t v = bsum[t * per + k];
       bsum[t * per + k] = run;
       run += v;
     }
-  if (t == 1023) cref[2 * n] = part[1023];
+  if (t == 1023) cref[2 * n] = run;  // the total
 }
 
 // cref[j] (exclusive scan of ref) from the block offsets and a block-local
@@ -307,81 +394,78 @@ __global__ __launch_bounds__(256) void seg_items_scan_kernel(uint32_t n, const u
 }
 
 
-// One thread per (perspective, position) j, after the scan and seg_items:
-// * a valid refresh gets its segment length (0 at every other j).  CHAIN: up
-//   to the next refresh of the same perspective (the next item; groups start
-//   with one).  STAR: the group's parent owns its children that are not
+// One thread per (perspective, position) j (grid stride), after the scan and
+// seg_items:
+// * a valid refresh gets its segment length (0 at every other j) and counts
+//   in the item histogram by (king block, length bin) — the king block rides
+//   in its refresh flag (seg_delta), so no position is decoded here.  CHAIN:
+//   up to the next refresh of the same perspective (the next item; groups
+//   start with one).  STAR: the group's parent owns its children that are not
 //   refreshes.
 // * any other position places its delta record at root + rank, so that a
 //   segment's records are contiguous.
+// At most one workgroup per CU: the histogram merge costs one global atomic
+// per non-empty bin per workgroup.
 template <class Fs>
-__global__ __launch_bounds__(256) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, uint32_t sbase,
-                                                        int star,
-                                                        const uint8_t* __restrict__ bucket,
-                                                        const uint32_t* __restrict__ ref,
-                                                        const uint32_t* __restrict__ cref,
-                                                        const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len,
-                                                        const uint4* __restrict__ dtmp, uint4* __restrict__ drec) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(1024) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, uint32_t sbase,
+                                                         int star,
+                                                         const uint8_t* __restrict__ bucket,
+                                                         const uint32_t* __restrict__ ref,
+                                                         const uint32_t* __restrict__ cref,
+                                                         const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len,
+                                                         const uint4* __restrict__ dtmp, uint4* __restrict__ drec,
+                                                         uint32_t* __restrict__ ctr) {
+  constexpr int kIB = SegCtr<Fs>::kIB;
+  __shared__ uint32_t h[kIB];
+  for (int t = threadIdx.x; t < kIB; t += blockDim.x) h[t] = 0;
+  __syncthreads();
   // Record 2n, read by items past the end of their segment: no rows, x row 2n
   // and bucket 0, i.e. x and PSQT stores just past the launch's buffer ranges
   // (dropped by the hardware), so the walk needs no liveness masking.
-  if (j == 0) drec[2 * n] = make_uint4(2 * n, Fs::kNone | Fs::kNone << 16, Fs::kNone | Fs::kNone << 16, 0u);
-  if (j >= 2 * n) return;
-  const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
-  if (ref[j]) {
-    uint32_t L = 0;
-    if (bucket[i] != 0xFF) {
-      if (star) {
-        const uint2 g = group_range(span, i, n, sbase);
-        L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
-      } else {
-        const uint32_t k = cref[j];
-        L = (k + 1 < cref[(c + 1) * n] ? ipos[k + 1] : n) - i;
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    drec[2 * n] = make_uint4(2 * n, Fs::kNone | Fs::kNone << 16, Fs::kNone | Fs::kNone << 16, 0u);
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < 2 * n; j += gridDim.x * blockDim.x) {
+    const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
+    const uint32_t rf = ref[j];
+    if (rf) {
+      uint32_t L = 0;
+      if (bucket[i] != 0xFF) {
+        if (star) {
+          const uint2 g = group_range(span, i, n, sbase);
+          L = i != g.x ? 1u : (g.y - i) - (cref[c * n + g.y] - cref[j + 1]);
+        } else {
+          const uint32_t k = cref[j];
+          L = (k + 1 < cref[(c + 1) * n] ? ipos[k + 1] : n) - i;
+        }
       }
+      len[j] = L;
+      if (L) atomicAdd(&h[((rf >> 8) & 0xFFu) * SegCtr<Fs>::kNB + seg_len_bin(L) * Fs::kClasses + (rf >> 16)], 1u);
+      continue;
     }
-    len[j] = L;
-    return;
+    len[j] = 0;
+    uint32_t r, rank;
+    if (star) {
+      r = group_range(span, i, n, sbase).x;  // the parent: a refresh item of this perspective
+      rank = (i - r) - (cref[j] - cref[c * n + r + 1]);
+    } else {
+      r = ipos[cref[j] - 1];  // the last refresh of this perspective before i (same game)
+      rank = i - r;
+    }
+    drec[c * n + r + rank] = dtmp[j];
   }
-  len[j] = 0;
-  uint32_t r, rank;
-  if (star) {
-    r = group_range(span, i, n, sbase).x;  // the parent: a refresh item of this perspective
-    rank = (i - r) - (cref[j] - cref[c * n + r + 1]);
-  } else {
-    r = ipos[cref[j] - 1];  // the last refresh of this perspective before i (same game)
-    rank = i - r;
-  }
-  drec[c * n + r + rank] = dtmp[j];
+  __syncthreads();
+  for (int t = threadIdx.x; t < kIB; t += blockDim.x)
+    if (h[t]) atomicAdd(&ctr[t], h[t]);
 }
 
 template <class Fs>
 __device__ __forceinline__ uint32_t seg_key(const typename Fs::Dec& d, int c, uint32_t L) {
-  return (uint32_t)Fs::block(c, c ? d.b.bk : d.b.wk) * 33u + seg_len_bin(L);
+  return (uint32_t)Fs::block(c, c ? d.b.bk : d.b.wk) * SegCtr<Fs>::kNB + seg_len_bin(L) * Fs::kClasses +
+         seg_count_class<Fs::kClasses>((uint32_t)d.nfeat);
 }
 
-// Both sort kernels run one thread per item k < cref[2n] (refresh of
+// The sort kernel runs one thread per item k < cref[2n] (refresh of
 // perspective k >= cref[n]); invalid positions are refreshes with len 0.
-template <class Fs>
-__global__ __launch_bounds__(1024) void seg_count_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
-                                                         const uint32_t* __restrict__ cref,
-                                                         const uint32_t* __restrict__ ipos,
-                                                         const uint32_t* __restrict__ len,
-                                                         uint32_t* __restrict__ ctr) {
-  constexpr int kIB = SegCtr<Fs>::kIB;
-  __shared__ uint32_t h[kIB];
-  for (int i = threadIdx.x; i < kIB; i += blockDim.x) h[i] = 0;
-  __syncthreads();
-  const uint32_t K = cref[2 * n], K0 = cref[n];
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < K; k += gridDim.x * blockDim.x) {
-    const uint32_t c = k >= K0 ? 1u : 0u, i = ipos[k], L = len[c * n + i];
-    if (L) atomicAdd(&h[seg_key<Fs>(Fs::decode(pos + i), (int)c, L)], 1u);
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kIB; i += blockDim.x)
-    if (h[i]) atomicAdd(&ctr[i], h[i]);
-}
-
 // Sorted item record: {root | half << 24 | bucket << 25, length, perspective,
 // list length + 1}; full feature list of the root as in the sliced plan.
 template <class Fs>
@@ -418,7 +502,8 @@ __global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Po
   const uint32_t slot = lbase[key] + rk;
   const uint32_t half = d.b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(d.b.cnt - 1) >> 2;
   items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)d.nfeat);
-  Fs::write_list(d, (int)c, slot, ctr, lists + threadIdx.x * kListStrideWords, flist);
+  const uint32_t pp = (slot - ctr[SegCtr<Fs>::kOff + (key / SegCtr<Fs>::kNB) * SegCtr<Fs>::kNB]) & 1u;  // parity in its king block
+  Fs::write_list(d, (int)c, slot, pp, lists + threadIdx.x * kListStrideWords, flist);
 }
 
 struct SegFetch {
@@ -747,7 +832,7 @@ template <class Fs>
 hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, uint32_t sbase, bool star,
                       const SlicedPlan& P, const SegPlan& G, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
   hipError_t e;
-  const uint32_t bs = 256, g1 = (n + bs - 1) / bs, g2 = (2 * n + bs - 1) / bs;
+  const uint32_t bs = 256, g1 = (n + bs - 1) / bs;
   if (g1 > kMaxScanBlocks) return hipErrorInvalidValue;
   uint32_t* bsum = static_cast<uint32_t*>(G.scan_temp);
   hipLaunchKernelGGL(seg_delta_kernel<Fs>, dim3(g1), dim3(bs), 0, stream, pos, n, sp, sbase, star ? 1 : 0, G.ref,
@@ -758,14 +843,12 @@ hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, 
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(seg_items_scan_kernel, dim3(g1, 2), dim3(256), 0, stream, n, G.ref, bsum, G.cref, G.ipos);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_place_kernel<Fs>, dim3(g2), dim3(bs), 0, stream, n, sp, sbase, star ? 1 : 0, bucket, G.ref,
-                     G.cref, G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
   uint32_t cb = (2 * n + 1023) / 1024;
   if (cb > 256) cb = 256;
-  hipLaunchKernelGGL(seg_count_kernel<Fs>, dim3(cb), dim3(1024), 0, stream, pos, n, G.cref, G.ipos, G.len, P.ctr);
+  hipLaunchKernelGGL(seg_place_kernel<Fs>, dim3(cb), dim3(1024), 0, stream, n, sp, sbase, star ? 1 : 0, bucket, G.ref,
+                     G.cref, G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec, P.ctr);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(plan_scan_kernel_t<Fs::KB>, dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
+  hipLaunchKernelGGL((plan_scan_kernel_t<Fs::KB, SegCtr<Fs>::kNB>), dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(seg_scatter_kernel<Fs>, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.cref,
                      G.ipos, G.len, P.ctr, (uint4*)G.items, P.flist);
@@ -777,6 +860,11 @@ hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, 
 // units close at kSegUnitPlies positions (>= 1 item each) or kUnitItems items;
 // a unit holding fewer than kSegUnitPlies / 160 items is its king block's last
 uint32_t seg_max_units(uint32_t chunk) { return 64 + (2 * chunk + kSegUnitPlies / 160 - 1) / (kSegUnitPlies / 160); }
+
+size_t seg_ctr_words() {
+  return std::max({SegCtr<ChessFs>::kWords, SegCtr<VariantFs<kVariantCrazyhouse>>::kWords,
+                   SegCtr<VariantFs<kVariantAtomic>>::kWords});
+}
 
 // the per-block refresh counts of seg_delta, two perspectives
 size_t seg_scan_temp_bytes(uint32_t chunk) { return (size_t)8 * ((chunk + 255) / 256 + 1); }

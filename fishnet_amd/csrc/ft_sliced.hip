@@ -40,7 +40,7 @@ __global__ __launch_bounds__(1024) void plan_count_kernel(const fnnue_pos* __res
   __syncthreads();
   uint32_t bad = 0;
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-    const LaneBoard b = lane_decode(pos + p);
+    const LaneBoard b = lane_decode<false>(pos + p);  // counts only: no occupancy mask
     if (!b.ok) {
       bad = 1;
       atomicAdd(&h[kItemBins + 8], 1u);
@@ -103,8 +103,8 @@ __global__ __launch_bounds__(kScatterPositions) void plan_scatter_kernel(const f
   const int bucket = (b.cnt - 1) >> 2;
   const uint32_t iw = lbase[kw] + rw, ib = lbase[kb] + rb;
   uint32_t* mine = lists + threadIdx.x * kListStrideWords;
-  write_rows(b, 0, b.wk, iw, ctr, mine, flist);
-  write_rows(b, 1, b.bk, ib, ctr, mine, flist);
+  write_rows(b, 0, b.wk, iw, (iw - ctr[kOff + king_block(0, b.wk) * 33]) & 1u, mine, flist);
+  write_rows(b, 1, b.bk, ib, (ib - ctr[kOff + king_block(1, b.bk) * 33]) & 1u, mine, flist);
   items[iw] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 0);
   items[ib] = ((uint32_t)b.cnt << 24) | ((uint32_t)bucket << 21) | (slot << 1) | (uint32_t)(b.stm != 1);
   bucket_out[slot] = (uint8_t)bucket;

@@ -110,6 +110,7 @@ struct SegPlan {
   size_t scan_temp_bytes;
 };
 size_t seg_scan_temp_bytes(uint32_t chunk);
+size_t seg_ctr_words();  // counter words of the segment plans (any feature set)
 uint32_t seg_max_units(uint32_t chunk);  // unit-table entries ft_segments may need
 // Once per grouped call: span[i] = {first, end} of position i's group
 // (absolute, npos entries; span == nullptr: check only).  check: the offsets

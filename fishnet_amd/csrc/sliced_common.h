@@ -106,6 +106,8 @@ __device__ __forceinline__ uint32_t nibble_bits(uint32_t z) {
   return (m | (m >> 12)) & 0xFFu;
 }
 
+// kOcc = false: the occupancy mask is not built (occ = 0; cnt still counts).
+template <bool kOcc = true>
 __device__ __forceinline__ LaneBoard lane_decode(const fnnue_pos* p) {
   LaneBoard b;
   const uint32_t* pw = reinterpret_cast<const uint32_t*>(p);
@@ -113,21 +115,24 @@ __device__ __forceinline__ LaneBoard lane_decode(const fnnue_pos* p) {
   for (int i = 0; i < 8; ++i) b.w[i] = pw[i];
   b.stm = (int)(pw[8] & 0xFF);
   b.occ = 0;
-  int nwk = 0, nbk = 0;
+  int nwk = 0, nbk = 0, cnt = 0;
   uint32_t bad = 0;
   b.wk = b.bk = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const uint32_t w = b.w[i];
-    b.occ |= (uint64_t)nibble_bits(~zero_nibbles(w) & 0x88888888u) << (8 * i);
+    const uint32_t occb = ~zero_nibbles(w) & 0x88888888u;  // bit 4k + 3: square 8i + k occupied
+    if constexpr (kOcc) b.occ |= (uint64_t)nibble_bits(occb) << (8 * i);
+    cnt += __popc(occb);
     const uint32_t kw = zero_nibbles(w ^ 0x66666666u), kb = zero_nibbles(w ^ 0xEEEEEEEEu);
     nwk += __popc(kw);
     nbk += __popc(kb);
     if (kw) b.wk = 8 * i + (__builtin_ctz(kw) >> 2);
     if (kb) b.bk = 8 * i + (__builtin_ctz(kb) >> 2);
-    bad |= zero_nibbles(w ^ 0x77777777u) | zero_nibbles(w ^ 0x88888888u) | zero_nibbles(~w);
+    // no piece codes 7, 15 (type 7: low three bits set) or 8 (black, no type)
+    bad |= (w & (w >> 1) & (w >> 2) & 0x11111111u) | zero_nibbles(w ^ 0x88888888u);
   }
-  b.cnt = __popcll(b.occ);
+  b.cnt = cnt;
   b.ok = !bad && nwk == 1 && nbk == 1 && b.cnt <= 32 && b.stm <= 1;
   return b;
 }
@@ -156,18 +161,29 @@ __host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
   return bin < 16 ? bin + 1 : bin < 32 ? 8 * bin - 104 : 160;
 }
 
+// Segment item bins per king block: 33 length bins x C classes of the root's
+// list length, so that the items of a pass, which all sum the pass's longest
+// list, have similar lengths (C = 4 for chess and atomic; 1 for crazyhouse,
+// whose lists count the pockets too and are nearly all full).
+template <int C>
+__host__ __device__ constexpr uint32_t seg_count_class(uint32_t nfeat) {
+  return C == 1 ? 0u : nfeat > 29 ? 3u : nfeat > 25 ? 2u : nfeat > 20 ? 1u : 0u;
+}
+
 // One workgroup of 1024 threads.  unit_items = 0: segment units (see
 // kSegUnitPlies) instead of fixed-size ones.  KB king blocks (32: chess; 64:
-// the variant feature sets), counters laid out as KB * 33 item bins + 9
+// the variant feature sets), counters laid out as KB * NB item bins + 9
 // position bins, then offsets, cursors and the unit count (kCnt / kOff / kCur
-// / kNUnits for KB = 32, kV* for 64).
-template <int KB>
+// / kNUnits for KB = 32, kV* for 64, SegCtr for segments).  NB = 33: bin =
+// list length (fixed-size units); NB = 33 C: bin = C * length bin + class.
+template <int KB, int NB = 33>
 __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel_t(uint32_t* __restrict__ ctr,
                                                                                   int4* __restrict__ units,
                                                                                   uint32_t unit_items) {
-  constexpr int kIB = KB * 33, kB = kIB + kPosBins, kO = kB, kC = 2 * kB, kNU = 3 * kB;
+  constexpr int kIB = KB * NB, kB = kIB + kPosBins, kO = kB, kC = 2 * kB, kNU = 3 * kB;
+  auto len_bin = [](int i) { return (i % NB) / (NB / 33); };
   __shared__ uint32_t s[kB];
-  __shared__ uint32_t part[1024];
+  __shared__ uint32_t part[16];
   const int t = threadIdx.x;
   // Exclusive scan of the item bins and, separately, of the position bins.
   constexpr int per = (kB + 1023) / 1024;
@@ -178,15 +194,19 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     local[k] = (i < kIB) ? ctr[i] : 0;
     sum += local[k];
   }
-  part[t] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const uint32_t v = t >= o ? part[t - o] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  // scan of the per-thread sums: inside each wave by shuffles, then over the
+  // 16 wave totals (one barrier instead of two per step of a block scan)
+  const int lane = t & 63, wv = t >> 6;
+  uint32_t incl = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
   }
-  uint32_t run = part[t] - sum;
+  if (lane == 63) part[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+  for (int w = 0; w < wv; ++w) run += part[w];
   for (int k = 0; k < per; ++k) {
     const int i = t * per + k;
     if (i < kIB) s[i] = run;
@@ -205,8 +225,7 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     ctr[kC + i] = s[i];
   }
   // end of king block kb's items
-  auto kb_end = [&](int kb) -> uint32_t { return kb == KB - 1 ? s[(KB - 1) * 33 + 32] + ctr[(KB - 1) * 33 + 32]
-                                                              : s[(kb + 1) * 33]; };
+  auto kb_end = [&](int kb) -> uint32_t { return kb == KB - 1 ? s[KB * NB - 1] + ctr[KB * NB - 1] : s[(kb + 1) * NB]; };
   if (unit_items == 0) {
     // Segment units: unit u of king block kb starts at the first item whose
     // cumulative positions (a bin's items counted at the bin's longest run)
@@ -216,14 +235,14 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     __shared__ uint32_t ubase[KB + 1];  // first unit of each king block
     for (int k = 0; k < per; ++k) {     // local[k] = count of bin t*per + k
       const int i = t * per + k;
-      if (i < kIB) pb[i] = local[k] * seg_bin_longest(i % 33);
+      if (i < kIB) pb[i] = local[k] * seg_bin_longest(len_bin(i));
     }
     __syncthreads();
     if (t < KB) {
       uint32_t run = 0;
-      for (int b = 0; b < 33; ++b) {
-        const uint32_t v = pb[t * 33 + b];
-        pb[t * 33 + b] = run;
+      for (int b = 0; b < NB; ++b) {
+        const uint32_t v = pb[t * NB + b];
+        pb[t * NB + b] = run;
         run += v;
       }
       const uint32_t mine = (run + kSegUnitPlies - 1) / kSegUnitPlies;
@@ -243,8 +262,8 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     for (int k = 0; k < per; ++k) {
       const int i = t * per + k;
       if (i >= kIB || local[k] == 0) continue;
-      const int kb = i / 33;
-      const uint32_t w = seg_bin_longest(i % 33), p0 = pb[i], p1 = p0 + local[k] * w;
+      const int kb = i / NB;
+      const uint32_t w = seg_bin_longest(len_bin(i)), p0 = pb[i], p1 = p0 + local[k] * w;
       for (uint32_t u = (p0 + kSegUnitPlies - 1) / kSegUnitPlies; u * kSegUnitPlies < p1; ++u)
         units[ubase[kb] + u] = make_int4(kb, (int)(s[i] + (u * kSegUnitPlies - p0 + w - 1) / w), 0, 0);
     }
@@ -260,7 +279,7 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     // Unit table: each king block's item range in chunks of <= unit_items;
     // lane kb counts its block's units, a wave prefix sum places them.
     const int kb = t;
-    const uint32_t b = s[kb * 33];
+    const uint32_t b = s[kb * NB];
     const uint32_t e = kb_end(kb);
     const uint32_t mine = (e - b + unit_items - 1) / unit_items;
     uint32_t incl = mine;
@@ -309,11 +328,10 @@ __host__ __device__ constexpr uint64_t plane_table(int persp) {
 // square, piece code and plane come from the bit position and a 64-bit plane
 // table instead of a 64-bit scan plus an 8-way word select per piece
 // (38 -> 18 VALU per piece).
-__device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ksq, uint32_t it,
-                                               const uint32_t* __restrict__ ctr, uint32_t* __restrict__ mine,
-                                               uint16_t* __restrict__ flist) {
-  const int kbc = king_block(persp, ksq);
-  const uint32_t pp = (it - ctr[kOff + kbc * 33]) & 1;
+// pp = the item's parity within its king block's items, (it - first item of
+// the block) & 1.
+__device__ __forceinline__ void write_rows(const LaneBoard& b, int persp, int ksq, uint32_t it, uint32_t pp,
+                                               uint32_t* __restrict__ mine, uint16_t* __restrict__ flist) {
   const uint32_t mirror = (ksq & 7) < 4 ? 1u : 0u;
   const uint32_t flip = (persp ? 56u : 0u) ^ (mirror ? 7u : 0u);
   const uint64_t ptab = persp ? plane_table(1) : plane_table(0);

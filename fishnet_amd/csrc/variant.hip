@@ -31,7 +31,7 @@ __global__ __launch_bounds__(1024) void vplan_count_kernel(const fnnue_vpos* __r
   __syncthreads();
   uint32_t bad = 0;
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
-    const VariantBoard v = vdecode(pos + p, pockets != 0);
+    const VariantBoard v = vdecode<false>(pos + p, pockets != 0);  // counts only: no occupancy mask
     if (!v.ok) {
       bad = 1;
       atomicAdd(&h[kVItemBins + 8], 1u);

@@ -16,9 +16,10 @@ struct VariantBoard {
   bool ok;
 };
 
+template <bool kOcc = true>
 __device__ __forceinline__ VariantBoard vdecode(const fnnue_vpos* p, bool pockets) {
   VariantBoard v;
-  v.b = lane_decode(reinterpret_cast<const fnnue_pos*>(p));
+  v.b = lane_decode<kOcc>(reinterpret_cast<const fnnue_pos*>(p));
   const uint8_t* h = reinterpret_cast<const uint8_t*>(p) + 33;
   int tot = 0;
   bool bad = false;
