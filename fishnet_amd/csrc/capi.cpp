@@ -276,14 +276,22 @@ int ensure_span(fnnue_ctx* c, size_t npos) {
   return FNNUE_OK;
 }
 
+// Records timing event k of a chunk (0: before the plan, 1: before the FT
+// main kernel, 2: before the stacks, 3: after them); FNNUE_TIMING_FT records
+// only events 1 and 2.
+int record_event(const fnnue_ctx* c, std::array<hipEvent_t, 4>* ev, int k, hipStream_t s) {
+  if (!ev || (c->timing == FNNUE_TIMING_FT && (k == 0 || k == 3))) return FNNUE_OK;
+  HIP_TRY(hipEventRecord((*ev)[k], s), "hipEventRecord");
+  return FNNUE_OK;
+}
+
 // Runs the stack kernel for [0, n) of the workspace and records timing.
 int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t s, std::array<hipEvent_t, 4>* ev,
                    const uint32_t* perm = nullptr, const int32_t* psqt_part = nullptr, int32_t* d_psqt = nullptr) {
-  if (ev) HIP_TRY(hipEventRecord((*ev)[2], s), "hipEventRecord");
+  if (int rc = record_event(c, ev, 2, s)) return rc;
   HIP_TRY(launch_stack(c->hd, c->x, c->bucket, n, c->ptrs, d_positional, perm, psqt_part, d_psqt, s),
           "stack kernel launch");
-  if (ev) HIP_TRY(hipEventRecord((*ev)[3], s), "hipEventRecord");
-  return FNNUE_OK;
+  return record_event(c, ev, 3, s);
 }
 
 // Workspace ordering across streams (the workspace is shared by every call on
@@ -572,7 +580,7 @@ int fnnue_net_accumulator_bound(const fnnue_net* net, int32_t* bound) {
 
 int fnnue_ctx_set_timing(fnnue_ctx* ctx, int enable) {
   if (!ctx) return fail(FNNUE_E_ARG, "null ctx");
-  ctx->timing = enable != 0;
+  ctx->timing = enable == FNNUE_TIMING_FT ? FNNUE_TIMING_FT : enable ? FNNUE_TIMING_ALL : FNNUE_TIMING_OFF;
   ctx->evused = 0;
   return FNNUE_OK;
 }
@@ -585,10 +593,11 @@ int fnnue_ctx_timing_phases(fnnue_ctx* ctx, uint32_t* launches, double* plan_ms,
   for (size_t i = 0; i < ctx->evused; ++i) {
     auto& e = ctx->evpool[i];
     float a = 0, b = 0, c = 0;
-    HIP_TRY(hipEventSynchronize(e[3]), "hipEventSynchronize");
-    HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]), "hipEventElapsedTime");
+    const bool all = ctx->timing != FNNUE_TIMING_FT;
+    HIP_TRY(hipEventSynchronize(all ? e[3] : e[2]), "hipEventSynchronize");
+    if (all) HIP_TRY(hipEventElapsedTime(&a, e[0], e[1]), "hipEventElapsedTime");
     HIP_TRY(hipEventElapsedTime(&b, e[1], e[2]), "hipEventElapsedTime");
-    HIP_TRY(hipEventElapsedTime(&c, e[2], e[3]), "hipEventElapsedTime");
+    if (all) HIP_TRY(hipEventElapsedTime(&c, e[2], e[3]), "hipEventElapsedTime");
     *plan_ms += a;
     *ft_ms += b;
     *stack_ms += c;
@@ -622,11 +631,11 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
     std::array<hipEvent_t, 4>* ev = nullptr;
     rc = next_events(ctx, &ev);
     if (rc) return rc;
-    if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+    if ((rc = record_event(ctx, ev, 0, s))) return rc;
     const uint32_t* perm = nullptr;
     const int32_t* psqt_part = nullptr;
     if (ctx->ft_impl == FNNUE_FT_GATHER) {
-      if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
+      if ((rc = record_event(ctx, ev, 1, s))) return rc;
       HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_scratch launch");
     } else {
@@ -673,14 +682,14 @@ int eval_groups_device(fnnue_ctx* ctx, const void* d_pos, size_t pos_bytes, cons
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, npos - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
     if ((rc = next_events(ctx, &ev))) return rc;
-    if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+    if ((rc = record_event(ctx, ev, 0, s))) return rc;
     if (sliced) {
       HIP_TRY(launch_ft_segments(ctx->hd, ctx->variant, pos + b * pos_bytes, m, span + b, (uint32_t)b, mode,
                                  ctx->ptrs, ctx->plan, ctx->seg, ctx->x, ctx->bucket, ctx->err, s, mid_event(ev)),
               "ft_segments launch");
       rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, nullptr, ctx->plan.psqt_part, d_psqt + b);
     } else {
-      if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
+      if ((rc = record_event(ctx, ev, 1, s))) return rc;
       HIP_TRY(launch_ft_groups(ctx->hd, static_cast<const fnnue_pos*>(d_pos), d_off, (uint32_t)ngroups, (uint32_t)b,
                                (uint32_t)(b + m), mode, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_groups launch");
@@ -724,10 +733,10 @@ int fnnue_eval_vpositions_device(fnnue_ctx* ctx, const fnnue_vpos* d_pos, size_t
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
     if ((rc = next_events(ctx, &ev))) return rc;
-    if (ev) HIP_TRY(hipEventRecord((*ev)[0], s), "hipEventRecord");
+    if ((rc = record_event(ctx, ev, 0, s))) return rc;
     HIP_TRY(launch_variant_plan(d_pos + b, m, ctx->variant, ctx->plan, d_psqt + b, ctx->bucket, ctx->err, s),
             "variant plan launch");
-    if (ev) HIP_TRY(hipEventRecord((*ev)[1], s), "hipEventRecord");
+    if ((rc = record_event(ctx, ev, 1, s))) return rc;
     HIP_TRY(launch_variant_ft(ctx->hd, ctx->variant, m, ctx->ptrs, ctx->plan, ctx->x, s), "variant ft launch");
     if ((rc = run_chunk_tail(ctx, m, d_positional + b, s, ev, ctx->plan.perm, ctx->plan.psqt_part, d_psqt + b)))
       return rc;

@@ -42,7 +42,7 @@ struct fnnue_ctx {
   int32_t acc_bound = 0;       // accumulator_bound of the net (SWAR rows allowed below 2^15)
   fnnue::SlicedPlan plan{};
   fnnue::SegPlan seg{};                // incremental sliced path for groups (allocated on first use)
-  bool timing = false;
+  int timing = 0;  // FNNUE_TIMING_*: 0 off, 1 every phase, 2 the FT main kernel only
   // per timed launch: before the FT plan, before the FT main kernel, before the
   // layer stacks, after them
   std::vector<std::array<hipEvent_t, 4>> evpool;

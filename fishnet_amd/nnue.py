@@ -336,8 +336,11 @@ class Evaluator:
     def set_swar(self, enable: bool) -> None:
         N.check(N.lib.fnnue_ctx_set_swar(self._h, 1 if enable else 0))
 
-    def set_timing(self, enable: bool) -> None:
-        N.check(N.lib.fnnue_ctx_set_timing(self._h, 1 if enable else 0))
+    def set_timing(self, enable, ft_only: bool = False) -> None:
+        """Events around every phase (plan / FT kernel / stacks), or with ft_only
+        only the two around the FT main kernel (FNNUE_TIMING_FT: each event
+        record costs the stream a few microseconds)."""
+        N.check(N.lib.fnnue_ctx_set_timing(self._h, (N.TIMING_FT if ft_only else N.TIMING_ALL) if enable else N.TIMING_OFF))
 
     def timing_phases(self) -> tuple[int, float, float, float]:
         """(timed launches, summed ms of the FT plan kernels, of the FT main kernel, of the layer stacks); resets."""

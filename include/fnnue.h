@@ -377,7 +377,15 @@ int fnnue_ctx_set_swar(fnnue_ctx *ctx, int enable);
  * chunk launched by a *_device call records events around the feature-
  * transformer kernel and the layer-stack kernel.  fnnue_ctx_timing_read
  * synchronises on the last event, returns the number of timed launches and the
- * summed kernel times (ms), and resets the accumulators. */
+ * summed kernel times (ms), and resets the accumulators.
+ * enable: FNNUE_TIMING_OFF (0), FNNUE_TIMING_ALL (1, any other non-zero value:
+ * four events per chunk, plan / FT kernel / stacks), FNNUE_TIMING_FT (2: only
+ * the two events around the FT main kernel; plan and stack times read 0).  An
+ * event record between two kernels costs the stream a few microseconds, so a
+ * throughput measurement times with FNNUE_TIMING_FT. */
+#define FNNUE_TIMING_OFF 0
+#define FNNUE_TIMING_ALL 1
+#define FNNUE_TIMING_FT 2
 int fnnue_ctx_set_timing(fnnue_ctx *ctx, int enable);
 int fnnue_ctx_timing_read(fnnue_ctx *ctx, uint32_t *launches, double *ft_ms, double *stack_ms);
 /* Same, split into the FT plan kernels, the FT main kernel (ft_slices /
