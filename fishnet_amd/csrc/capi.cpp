@@ -240,7 +240,9 @@ int next_events(fnnue_ctx* c, std::array<hipEvent_t, 4>** out) {
   if (!c->timing) return FNNUE_OK;
   if (c->evused == c->evpool.size()) {
     std::array<hipEvent_t, 4> quad{nullptr, nullptr, nullptr, nullptr};
-    for (auto& e : quad) HIP_TRY(hipEventCreate(&e), "hipEventCreate");
+    // timing only: no system-scope fence (an L2 write-back per record, which
+    // the stream waits for between two kernels)
+    for (auto& e : quad) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence), "hipEventCreate");
     c->evpool.push_back(quad);
   }
   *out = &c->evpool[c->evused++];
