@@ -297,20 +297,34 @@ int run_chunk_tail(fnnue_ctx* c, uint32_t n, int32_t* d_positional, hipStream_t 
 }
 
 // Workspace ordering across streams (the workspace is shared by every call on
-// a ctx): each *_device call first waits for the event the previous call
-// recorded on its own stream, and records the event on its stream when its
-// work is enqueued (also after an error: part of it may be).  No stream handle
-// of an earlier call is ever used again, so a caller may destroy a stream
-// right after a call on it.
+// a ctx): a call on a caller's stream records ws_event on it when its work is
+// enqueued (also after an error: part of it may be), and each call first
+// waits for that event.  No caller stream handle of an earlier call is ever
+// used again, so a caller may destroy a stream right after a call on it.  A
+// call on the context's own stream records nothing (an event record between
+// two kernels idles the stream for microseconds): the next call on the same
+// stream is ordered by the stream, and a call on another stream records
+// ws_event on the own stream, which lives as long as the context, first.
 struct WorkspaceUse {
   fnnue_ctx* c;
   hipStream_t s;
   ~WorkspaceUse() {
-    if (hipEventRecord(c->ws_event, s) == hipSuccess) c->ws_recorded = true;
+    if (s == c->stream) {
+      c->ws_own_pending = true;
+    } else if (hipEventRecord(c->ws_event, s) == hipSuccess) {
+      c->ws_recorded = true;
+      c->ws_own_pending = false;
+    }
   }
 };
 
 int order_workspace(fnnue_ctx* c, hipStream_t s) {
+  if (c->ws_own_pending) {
+    if (s == c->stream) return FNNUE_OK;
+    HIP_TRY(hipEventRecord(c->ws_event, c->stream), "hipEventRecord");
+    c->ws_recorded = true;
+    c->ws_own_pending = false;
+  }
   if (c->ws_recorded) HIP_TRY(hipStreamWaitEvent(s, c->ws_event, 0), "hipStreamWaitEvent");
   return FNNUE_OK;
 }

@@ -310,7 +310,9 @@ hipError_t relayout_g(const NetPtrs& net, void* tiles, hipStream_t stream) {
 }  // namespace
 
 size_t sliced_tiles_bytes(uint32_t hd) { return tile_uint4_count(hd) * sizeof(uint4); }
-size_t sliced_ctr_words() { return 3 * kBins + 16; }
+// a multiple of 4 words: hipMemsetAsync of a size that is not a multiple of
+// 16 bytes runs two fill kernels
+size_t sliced_ctr_words() { return (3 * kBins + 16 + 3) & ~(size_t)3; }
 uint32_t sliced_max_units(uint32_t chunk) { return 32 + (2 * chunk + kUnitItems - 1) / kUnitItems; }
 
 #define FNNUE_HD_DISPATCH(hd, CALL) \

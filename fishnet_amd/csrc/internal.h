@@ -52,6 +52,10 @@ struct fnnue_ctx {
   // previous call on its stream) and records ws_event on its own stream.
   hipEvent_t ws_event = nullptr;
   bool ws_recorded = false;
+  // The last call ran on `stream` (the context's own, which lives as long as
+  // the context) and recorded no event: a call on the same stream needs no
+  // ordering, one on another stream records ws_event on `stream` first.
+  bool ws_own_pending = false;
 };
 
 

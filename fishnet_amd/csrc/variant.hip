@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kScatterPositions) void vplan_scatter_kernel(
 
 }  // namespace
 
-size_t variant_ctr_words() { return 3 * kVBins + 16; }
+size_t variant_ctr_words() { return (3 * kVBins + 16 + 3) & ~(size_t)3; }  // a multiple of 4 words (one fill kernel)
 uint32_t variant_max_units(uint32_t chunk) { return 64 + (2 * chunk + kUnitItems - 1) / kUnitItems; }
 
 hipError_t launch_variant_plan(const fnnue_vpos* pos, uint32_t n, int variant, const SlicedPlan& P, int32_t* psqt,

@@ -413,6 +413,32 @@ def test_device_calls_on_two_streams(ev_cache):
         assert np.array_equal(ps.cpu().numpy()[idx], ops) and np.array_equal(po.cpu().numpy()[idx], opo)
 
 
+def test_device_calls_own_stream_then_other_stream(ev_cache):
+    """Calls on the context's own stream record no workspace event; a following
+    call on another stream (no sync in between) records it on the own stream
+    first and waits for it, and a call on the own stream after that waits for
+    the other stream's event: own -> other -> own -> own, all results exact."""
+    import torch
+    ev, on = ev_cache()
+    batches = [F.random_playouts(51 + k, 150_000, threads=8) for k in range(4)]
+    dev = torch.device("cuda", 0)
+    s2 = torch.cuda.Stream(dev)
+    ds = [torch.from_numpy(b).to(dev) for b in batches]
+    outs = [torch.zeros(len(b), dtype=torch.int32, device=dev) for b in batches for _ in range(2)]
+    torch.cuda.synchronize()
+    for k, stream in enumerate((None, s2.cuda_stream, None, None)):
+        ev.eval_positions_device(ds[k].data_ptr(), len(batches[k]), outs[2 * k].data_ptr(), outs[2 * k + 1].data_ptr(),
+                                 stream)
+    ev.check()
+    torch.cuda.synchronize()
+    for k, pos in enumerate(batches):
+        idx = np.arange(k, len(pos), 11)
+        ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+        assert rc == 0
+        assert np.array_equal(outs[2 * k].cpu().numpy()[idx], ops)
+        assert np.array_equal(outs[2 * k + 1].cpu().numpy()[idx], opo)
+
+
 def test_device_call_after_its_stream_was_destroyed(ev_cache):
     """A *_device call on a temporary stream, the stream destroyed right after,
     then calls on the context's own stream and on another stream: the library
@@ -590,3 +616,31 @@ def test_real_net_file_matches_oracle():
                           "positions": len(pos), "plies": len(gpos), "mismatches": 0}))
     finally:
         ev.close()
+
+
+def test_timing_modes(ev_cache):
+    """fnnue_ctx_set_timing: FNNUE_TIMING_ALL times plan / FT kernel / stacks of
+    every chunk; FNNUE_TIMING_FT records only the two events around the FT
+    kernel (plan and stack read 0); off records nothing.  Results unchanged."""
+    import torch
+    ev, on = ev_cache()
+    pos = F.random_playouts(61, 100_000, threads=8)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(pos).to(dev)
+    ps, po = (torch.zeros(len(pos), dtype=torch.int32, device=dev) for _ in range(2))
+    torch.cuda.synchronize()
+    for mode in ("all", "ft", "off"):
+        ev.set_timing(mode != "off", ft_only=mode == "ft")
+        for _ in range(3):
+            ev.eval_positions_device(d.data_ptr(), len(pos), ps.data_ptr(), po.data_ptr(), None)
+        ev.check()
+        n, plan, ft, stack = ev.timing_phases()
+        if mode == "off":
+            assert n == 0 and plan == ft == stack == 0
+        else:
+            assert n == 3 and ft > 0
+            assert (plan > 0 and stack > 0) if mode == "all" else (plan == 0 and stack == 0)
+    ev.set_timing(False)
+    idx = np.arange(0, len(pos), 17)
+    ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+    assert rc == 0 and np.array_equal(ps.cpu().numpy()[idx], ops) and np.array_equal(po.cpu().numpy()[idx], opo)
