@@ -650,12 +650,20 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ 
   for (int a = 0; a < kAhead; ++a) next[a] = fetch(8 * a + 1 + q);
   u16x4 blo = lo, bhi = hi;
   int32_t pb = p;
-  // The 8 positions of a batch, straight-line; kAdd2 as in apply_delta.
-  auto run_batch = [&](auto add2) {
-    constexpr bool kAdd2 = decltype(add2)::value;
+  // Positions in the last batch (1..8, wave-uniform): the walk stops at the
+  // pass's longest segment instead of rounding it up to whole batches (even
+  // lengths dominate CHAIN segments in random games — a king moves every
+  // other ply — and 23 % of the position steps of config 3 were past every
+  // item's end).
+  const uint32_t rest = maxL - 1 - 8 * (nb - 1);
+  // The positions of a batch, straight-line; kAdd2 as in apply_delta; kLast:
+  // only the first `rest` (uniform branches).
+  auto run_batch = [&](auto add2, auto last) {
+    constexpr bool kAdd2 = decltype(add2)::value, kLast = decltype(last)::value;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const uint4 d = db[jj];  // past the segment's end: the sentinel record (seg_members_kernel)
+      if (kLast && jj > 0 && (uint32_t)jj >= rest) break;
+      const uint4 d = db[jj];  // past the segment's end: the sentinel record (seg_place_kernel)
       apply_delta<kAdd2, kSwar>(lbase, d, blo, bhi, lo, hi);
       const uint32_t xo = (d.x & kRowMask) * (HD / 2) + col;
       __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc, xo, 0, 0);
@@ -679,10 +687,18 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ 
     next[kAhead - 1] = fetch(8 * (b + kAhead) + 1 + q);
     db[q] = batch;  // LDS ops of a wave complete in order: read below, overwritten next batch
     // lane q of an item holds record 8b+1+q: any with a second add?
-    if (__ballot((batch.z >> 16) != kNone))
-      run_batch(std::true_type{});
-    else
-      run_batch(std::false_type{});
+    const bool add2 = __ballot((batch.z >> 16) != kNone) != 0;
+    if (b + 1 < nb) {
+      if (add2)
+        run_batch(std::true_type{}, std::false_type{});
+      else
+        run_batch(std::false_type{}, std::false_type{});
+    } else {
+      if (add2)
+        run_batch(std::true_type{}, std::true_type{});
+      else
+        run_batch(std::false_type{}, std::true_type{});
+    }
   }
 }
 
