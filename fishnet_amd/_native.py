@@ -120,6 +120,7 @@ SIGNATURES = {
     "fnnue_game_vpositions": ([_i32, C.c_char_p, C.c_char_p, _vp, _sz, _P(_sz)], _i32),
     "fnnue_game_vchildren": ([_i32, C.c_char_p, C.c_char_p, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_vperft": ([_i32, C.c_char_p, _i32, _P(_u64)], _i32),
+    "fnnue_game_end": ([_i32, C.c_char_p, C.c_char_p, _P(_i32)], _i32),
     "fnnue_random_vgame": ([_u64, _i32, C.c_char_p, _u32, C.c_char_p, _sz, _P(_sz)], _i32),
     "fnnue_random_vgames": ([_u64, _i32, _sz, _u32, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz)], _i32),
     "fnnue_build_vbatch_device": ([_vp, _i32, _vp, _vp, _vp, _sz, _i32, _vp, _sz, _vp, _sz, _P(_sz), _P(_sz), _vp],
@@ -132,6 +133,7 @@ SIGNATURES = {
     "fnnue_eval_vgroups_device": ([_vp, _vp, _vp, _sz, _sz, _i32, _vp, _vp, _vp], _i32),
     # include/fnnue_backend.h
     "fnnue_backend_channel": ([_vp, _i32, _vp, _P(_vp)], _i32),
+    "fnnue_backend_channel_nets": ([_vp, _i32, _vp, _P(_vp)], _i32),
     "fnnue_backend_free": ([_vp], None),
     "fnnue_backend_batch_size": ([_vp, _P(_sz)], _i32),
     "fnnue_backend_go": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp], _i32),

@@ -169,11 +169,23 @@ class GpuEvalStub:
         return r
 
 
-def channel(net, device: int = 0, normalize_to_pawn: int = 0) -> tuple[GpuEvalStub, GpuEvalActor]:
-    """stockfish::channel for the GPU evaluator (net: fishnet_amd.Net)."""
+class _Nets(C.Structure):
+    _fields_ = [("chess", C.c_void_p), ("crazyhouse", C.c_void_p), ("atomic", C.c_void_p)]
+
+
+def channel(net=None, device: int = 0, normalize_to_pawn: int = 0, *, crazyhouse=None,
+            atomic=None) -> tuple[GpuEvalStub, GpuEvalActor]:
+    """stockfish::channel for the GPU evaluator.  `net` (a fishnet_amd.Net)
+    goes to the slot of its variant; `crazyhouse` / `atomic` add variant nets
+    (fnnue_backend_channel_nets): each batch is evaluated by its variant's net."""
     h = C.c_void_p()
     init = _Init(normalize_to_pawn, 0)
-    N.check(N.lib.fnnue_backend_channel(net._h, device, C.byref(init), C.byref(h)))
+    if crazyhouse is None and atomic is None:
+        N.check(N.lib.fnnue_backend_channel(net._h, device, C.byref(init), C.byref(h)))
+    else:
+        nets = _Nets(net._h if net is not None else None, crazyhouse._h if crazyhouse is not None else None,
+                     atomic._h if atomic is not None else None)
+        N.check(N.lib.fnnue_backend_channel_nets(C.byref(nets), device, C.byref(init), C.byref(h)))
     actor = GpuEvalActor(h)
     return GpuEvalStub(actor), actor
 

@@ -4,7 +4,8 @@
 // is a bounded mpsc channel (capacity 1) into an actor owning one engine
 // process; StockfishStub::go sends a Position with a oneshot callback and
 // maps any failure to PositionFailed{batch_id}.  Here the actor is a worker
-// thread owning one fnnue_ctx; a message carries whole acquired batches
+// thread owning one fnnue_ctx per net (chess, and optionally the crazyhouse
+// and atomic variant nets); a message carries whole acquired batches
 // (AcquireResponseBody, [ref] src/api.rs:293-309), expanded the way
 // IncomingBatch::from_acquired does ([ref] src/queue.rs:518-627) — but on the
 // device: the FEN/UCI text goes to HBM once, the builder replays every game
@@ -24,6 +25,7 @@
 #include "board.h"
 #include "builder.h"
 #include "internal.h"
+#include "vboard.h"
 
 using namespace fnnue;
 using namespace fnnue::detail;
@@ -31,6 +33,7 @@ using namespace fnnue::detail;
 namespace {
 
 constexpr int32_t kNormalizeToPawnSf151 = 361;  // upstream uci.h NormalizeToPawnValue (SF 15.1, recalled)
+constexpr int kKinds = 3;                       // net slots: kVariantChess, kVariantCrazyhouse, kVariantAtomic
 
 // One message on the channel: StockfishMessage::Go with its callback.
 struct Job {
@@ -80,11 +83,18 @@ size_t count_moves(const char* s) {
   return n;
 }
 
-// Variants this backend evaluates with the chess net (EngineFlavor::Official,
-// queue.rs:530-539); everything else the reference sends to Fairy-Stockfish.
-bool chess_variant(const char* v) {
-  return !v || !*v || !std::strcmp(v, "standard") || !std::strcmp(v, "chess960") ||
-         !std::strcmp(v, "fromPosition") || !std::strcmp(v, "chess");
+// The net slot of a batch's variant (shakmaty Variant names, [ref]
+// src/api.rs:304; logger.rs:194-201): standard chess (EngineFlavor::Official
+// for analysis, queue.rs:530-539) and the two variants with a Fairy-Stockfish
+// NNUE feature set here.  -1: a variant this backend does not evaluate
+// (antichess, horde, kingOfTheHill, racingKings, threeCheck).
+int kind_of(const char* v) {
+  if (!v || !*v || !std::strcmp(v, "standard") || !std::strcmp(v, "chess960") || !std::strcmp(v, "fromPosition") ||
+      !std::strcmp(v, "chess"))
+    return kVariantChess;
+  if (!std::strcmp(v, "crazyhouse")) return kVariantCrazyhouse;
+  if (!std::strcmp(v, "atomic")) return kVariantAtomic;
+  return -1;
 }
 
 int64_t to_cp(int32_t psqt, int32_t positional, int32_t norm) {
@@ -92,24 +102,106 @@ int64_t to_cp(int32_t psqt, int32_t positional, int32_t norm) {
   return v * 100 / norm;
 }
 
+// A root with no legal move: the engine prints `info depth 0 score mate 0`
+// (checkmated; atomic: its king exploded) or `score cp 0` (stalemate) and
+// `bestmove (none)` ([ref] src/stockfish.rs:359-376, 418-425: Score::Mate(0)
+// / Score::Cp(0), best_move None, nodes 0).
+void terminal_response(fnnue_position_response& r, uint8_t fin) {
+  r.score_kind = (fin & (kFinalCheck | kFinalExtinct)) ? FNNUE_SCORE_MATE : FNNUE_SCORE_CP;
+  r.score = 0;
+  r.depth = 0;
+  r.nodes = 0;
+  r.best_move[0] = 0;
+}
+
+// Host replay of a move batch's root (Work::Move: the position after all
+// moves), with its legal children and their game-end flags.
+struct MoveRoot {
+  uint8_t fin = 0;                 // kFinal* of the root
+  std::vector<std::string> uci;    // legal moves
+  std::vector<uint8_t> kid_fin;    // kFinal* of each child
+};
+
+int chess_move_root(const fnnue_acquired& a, MoveRoot& R, std::vector<fnnue_pos>& kids) {
+  Board b;
+  std::string e;
+  if (!board_from_fen(a.position ? a.position : "", b, &e)) return FNNUE_E_FEN;
+  std::string tok;
+  for (const char* p = a.moves ? a.moves : "";; ++p) {
+    if (*p && *p != ' ' && *p != '\t' && *p != '\n' && *p != '\r') {
+      tok += *p;
+      continue;
+    }
+    if (!tok.empty()) {
+      Move m;
+      if (!parse_uci(b, tok.c_str(), m)) return FNNUE_E_MOVE;
+      b.do_move(m);
+      tok.clear();
+    }
+    if (!*p) break;
+  }
+  auto fin_of = [](const Board& x, const std::vector<Move>& ms) {
+    return (uint8_t)((ms.empty() ? kFinalNoMoves : 0) | (x.in_check() ? kFinalCheck : 0));
+  };
+  std::vector<Move> ms, km;
+  b.legal_moves(ms);
+  R.fin = fin_of(b, ms);
+  for (const Move& m : ms) {
+    Board k = b;
+    k.do_move(m);
+    k.legal_moves(km);
+    kids.push_back(k.pack());
+    R.uci.push_back(b.uci(m, b.chess960));
+    R.kid_fin.push_back(fin_of(k, km));
+  }
+  return FNNUE_OK;
+}
+
+int variant_move_root(int variant, const fnnue_acquired& a, MoveRoot& R, std::vector<fnnue_vpos>& kids) {
+  vb::VBoard b;
+  const char* fen = a.position ? a.position : "";
+  if (!vb::parse_fen(fen, 0, (uint32_t)std::strlen(fen), variant, b)) return FNNUE_E_FEN;
+  const char* mv = a.moves ? a.moves : "";
+  const uint32_t end = (uint32_t)std::strlen(mv);
+  uint32_t p = 0, st;
+  int len;
+  while ((len = vb::next_token(mv, p, end, st)) > 0) {
+    vb::VMove m;
+    if (!vb::match_uci(b, mv + st, len, m)) return FNNUE_E_MOVE;
+    vb::do_move(b, m);
+  }
+  R.fin = vb::final_state(b);
+  vb::for_each_legal(b, [&](const vb::VMove& m) -> bool {
+    vb::VBoard k = b;
+    vb::do_move(k, m);
+    kids.push_back(vb::pack(k));
+    R.uci.push_back(vb::vuci(b, m));
+    R.kid_fin.push_back(vb::final_state(k));
+    return true;
+  });
+  return FNNUE_OK;
+}
+
 }  // namespace
 
 struct fnnue_backend {
-  fnnue_ctx* ctx = nullptr;
+  fnnue_ctx* ctx[kKinds] = {};  // one evaluator per net, all on one device
+  int device = 0;
   int32_t norm = kNormalizeToPawnSf151;
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;  // slot / done / stop changes
   Job* slot = nullptr;         // the capacity-1 channel
   bool stop = false;
-  DevBuf text, fen_off, mv_off, pos, goff, psqt, positional;
-  std::vector<fnnue_pos> hpos;
+  DevBuf text, fen_off, mv_off, pos, goff, psqt, positional, fin;
+  std::vector<uint8_t> hpos;  // positions read back to find an invalid one (36 or 48 B records)
   std::vector<int32_t> hpsqt, hpositional;
   std::vector<uint32_t> hgoff;
+  std::vector<uint8_t> hfin;
 
   void run(Job& j);
-  int analysis(Job& j, const std::vector<size_t>& games, std::vector<size_t>& base);
-  int moves(Job& j, const std::vector<size_t>& games);
+  int analysis(Job& j, int kind, const std::vector<size_t>& games, const std::vector<uint8_t>& skip);
+  int moves(Job& j, int kind, const std::vector<size_t>& games);
   void loop() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
@@ -128,14 +220,17 @@ struct fnnue_backend {
   }
 };
 
-// Analysis batches: the games' text to HBM, the device builder replays them
-// (one CHAIN group per game), CHAIN evaluation, results back.  A game the
-// builder rejects (FEN / move) or whose positions the evaluator rejects fails
-// its own batch only: it is dropped and the rest rebuilt.  base[i] = first
-// position of games[i] in the host result arrays.
-int fnnue_backend::analysis(Job& j, const std::vector<size_t>& games_in, std::vector<size_t>& base) {
+// Analysis batches of one net: the games' text to HBM, the device builder
+// replays them (one CHAIN group per game) and flags each game's last
+// position, CHAIN evaluation, responses written in place.  A game the builder
+// rejects (FEN / move) or whose positions the evaluator rejects fails its own
+// batch only: it is dropped and the rest rebuilt.
+int fnnue_backend::analysis(Job& j, int kind, const std::vector<size_t>& games_in, const std::vector<uint8_t>& skip) {
+  fnnue_ctx* c = ctx[kind];
+  const bool chess = kind == kVariantChess;
+  const size_t rec = chess ? sizeof(fnnue_pos) : sizeof(fnnue_vpos);
   std::vector<size_t> live = games_in;
-  hipStream_t s = ctx->stream;
+  hipStream_t s = c->stream;
   while (!live.empty()) {
     std::string t;
     std::vector<uint32_t> fo(live.size() + 1), mo(live.size());
@@ -153,6 +248,7 @@ int fnnue_backend::analysis(Job& j, const std::vector<size_t>& games_in, std::ve
     if (int rc = text.reserve(t.size() + 1)) return rc;
     if (int rc = fen_off.reserve(fo.size() * 4)) return rc;
     if (int rc = mv_off.reserve(mo.size() * 4)) return rc;
+    if (int rc = fin.reserve(ng)) return rc;
     HIP_TRY(hipMemcpyAsync(text.p, t.data(), t.size(), hipMemcpyHostToDevice, s), "H2D(text)");
     HIP_TRY(hipMemcpyAsync(fen_off.p, fo.data(), fo.size() * 4, hipMemcpyHostToDevice, s), "H2D(fen offsets)");
     HIP_TRY(hipMemcpyAsync(mv_off.p, mo.data(), mo.size() * 4, hipMemcpyHostToDevice, s), "H2D(move offsets)");
@@ -167,41 +263,52 @@ int fnnue_backend::analysis(Job& j, const std::vector<size_t>& games_in, std::ve
       live.erase(live.begin() + (long)R.err_game);
       return (int)FNNUE_OK;
     };
+    auto build = [&](void* out, size_t cap, uint32_t* goffp, size_t ocap) {
+      return chess ? build_batch_device(text.as<char>(), fen_off.as<uint32_t>(), mv_off.as<uint32_t>(), ng, false,
+                                        static_cast<fnnue_pos*>(out), cap, goffp, ocap, s, fin.as<uint8_t>())
+                   : build_vbatch_device(kind, text.as<char>(), fen_off.as<uint32_t>(), mv_off.as<uint32_t>(), ng,
+                                         false, static_cast<fnnue_vpos*>(out), cap, goffp, ocap, s,
+                                         fin.as<uint8_t>());
+    };
     // sizing pass, then the outputs (both synchronise the stream)
-    BuildResult R = build_batch_device(text.as<char>(), fen_off.as<uint32_t>(), mv_off.as<uint32_t>(), ng, false,
-                                       nullptr, 0, nullptr, 0, s);
+    BuildResult R = build(nullptr, 0, nullptr, 0);
     if (R.hip != hipSuccess) return hip_fail(R.hip, "device batch builder");
     if (R.err_code) {
       if (int rc = drop(R)) return rc;
       continue;
     }
     const size_t n = R.n_out;
-    if (int rc = pos.reserve(n * sizeof(fnnue_pos))) return rc;
+    if (int rc = pos.reserve(n * rec)) return rc;
     if (int rc = goff.reserve((ng + 1) * 4)) return rc;
     if (int rc = psqt.reserve(n * 4)) return rc;
     if (int rc = positional.reserve(n * 4)) return rc;
-    R = build_batch_device(text.as<char>(), fen_off.as<uint32_t>(), mv_off.as<uint32_t>(), ng, false,
-                           pos.as<fnnue_pos>(), n, goff.as<uint32_t>(), ng + 1, s);
+    R = build(pos.p, n, goff.as<uint32_t>(), ng + 1);
     if (R.hip != hipSuccess) return hip_fail(R.hip, "device batch builder");
     if (R.err_code) {
       if (int rc = drop(R)) return rc;
       continue;
     }
     if (R.capacity || R.n_out != n || R.n_groups != ng) return fail(FNNUE_E_DEVICE, "batch builder sizes changed");
-    int rc = fnnue_eval_groups_device(ctx, pos.as<fnnue_pos>(), goff.as<uint32_t>(), ng, n, FNNUE_GROUP_CHAIN,
-                                      psqt.as<int32_t>(), positional.as<int32_t>(), s);
-    if (rc == FNNUE_OK) rc = fnnue_ctx_check(ctx);  // synchronises; latched invalid positions
+    int rc = chess ? fnnue_eval_groups_device(c, pos.as<fnnue_pos>(), goff.as<uint32_t>(), ng, n, FNNUE_GROUP_CHAIN,
+                                              psqt.as<int32_t>(), positional.as<int32_t>(), s)
+                   : fnnue_eval_vgroups_device(c, pos.as<fnnue_vpos>(), goff.as<uint32_t>(), ng, n, FNNUE_GROUP_CHAIN,
+                                               psqt.as<int32_t>(), positional.as<int32_t>(), s);
+    if (rc == FNNUE_OK) rc = fnnue_ctx_check(c);  // synchronises; latched invalid positions
     hgoff.resize(ng + 1);
     HIP_TRY(hipMemcpy(hgoff.data(), goff.p, (ng + 1) * 4, hipMemcpyDeviceToHost), "D2H(group offsets)");
     if (rc == FNNUE_E_POSITION) {
       // A FEN the builder parses but the evaluator cannot (kings, > 32
       // pieces): find the games holding such positions, fail those batches.
-      hpos.resize(n);
-      HIP_TRY(hipMemcpy(hpos.data(), pos.p, n * sizeof(fnnue_pos), hipMemcpyDeviceToHost), "D2H(positions)");
+      hpos.resize(n * rec);
+      HIP_TRY(hipMemcpy(hpos.data(), pos.p, n * rec, hipMemcpyDeviceToHost), "D2H(positions)");
       std::vector<size_t> keep;
       for (size_t g = 0; g < ng; ++g) {
         bool ok = true;
-        for (uint32_t k = hgoff[g]; k < hgoff[g + 1] && ok; ++k) ok = valid_host_pos(hpos[k]);
+        for (uint32_t k = hgoff[g]; k < hgoff[g + 1] && ok; ++k) {
+          const uint8_t* p = hpos.data() + (size_t)k * rec;
+          ok = chess ? valid_host_pos(*reinterpret_cast<const fnnue_pos*>(p))
+                     : host_vpos_state(*reinterpret_cast<const fnnue_vpos*>(p), kind) != 0;
+        }
         if (ok)
           keep.push_back(live[g]);
         else
@@ -214,85 +321,94 @@ int fnnue_backend::analysis(Job& j, const std::vector<size_t>& games_in, std::ve
     if (rc) return rc;
     hpsqt.resize(n);
     hpositional.resize(n);
+    hfin.resize(ng);
     HIP_TRY(hipMemcpy(hpsqt.data(), psqt.p, n * 4, hipMemcpyDeviceToHost), "D2H(psqt)");
     HIP_TRY(hipMemcpy(hpositional.data(), positional.p, n * 4, hipMemcpyDeviceToHost), "D2H(positional)");
+    HIP_TRY(hipMemcpy(hfin.data(), fin.p, ng, hipMemcpyDeviceToHost), "D2H(final flags)");
     for (size_t g = 0; g < ng; ++g) {
       const size_t i = live[g];
-      const size_t expect = j.off[i + 1] - j.off[i];
-      if (hgoff[g + 1] - hgoff[g] != expect) return fail(FNNUE_E_DEVICE, "builder ply count differs from the moves");
-      base[i] = hgoff[g];
+      const uint32_t b = j.off[i], len = j.off[i + 1] - b;
+      if (hgoff[g + 1] - hgoff[g] != len) return fail(FNNUE_E_DEVICE, "builder ply count differs from the moves");
+      for (uint32_t k = 0; k < len; ++k) {
+        fnnue_position_response& r = j.out[b + k];
+        if (skip[b + k]) continue;
+        const size_t x = hgoff[g] + k;
+        r.matrix = j.batches[i].multipv > 0 ? 1 : 0;  // Work::matrix_wanted: multipv is Some
+        r.psqt = hpsqt[x];
+        r.positional = hpositional[x];
+        r.score_kind = FNNUE_SCORE_CP;
+        r.score = to_cp(r.psqt, r.positional, norm);
+        r.depth = 0;
+        r.nodes = 1;
+      }
+      // The last ply is the only one that can have no legal move (nothing can
+      // be played from it): mate 0 / cp 0 instead of an evaluation.
+      if (len && (hfin[g] & kFinalNoMoves) && !skip[b + len - 1]) terminal_response(j.out[b + len - 1], hfin[g]);
     }
     return FNNUE_OK;
   }
   return FNNUE_OK;
 }
 
-// Move batches: the position after all moves (host replay: one position per
-// batch), its legal children evaluated from scratch, best = argmax -v(child).
-int fnnue_backend::moves(Job& j, const std::vector<size_t>& games) {
+// Move batches of one net: the position after all moves (host replay: one
+// position per batch) and its legal children.  A one-ply search: a child that
+// mates (checkmate, or atomic: the other king exploded) wins outright (score
+// mate 1), a stalemating child is a draw (0), every other child is worth
+// -v(child) from its NNUE evaluation; best = the first maximum.  A root with
+// no legal move answers as the engine does: no best move, mate 0 / cp 0.
+int fnnue_backend::moves(Job& j, int kind, const std::vector<size_t>& games) {
   struct Cand {
     size_t batch;
-    std::vector<std::string> uci;
+    MoveRoot root;
     size_t first;
   };
   std::vector<Cand> cands;
   std::vector<fnnue_pos> kids;
+  std::vector<fnnue_vpos> vkids;
   for (size_t i : games) {
-    const fnnue_acquired& a = j.batches[i];
-    Board b;
-    std::string e;
-    if (!board_from_fen(a.position ? a.position : "", b, &e)) {
-      j.rc[i] = FNNUE_E_FEN;
+    Cand c{i, {}, kind == kVariantChess ? kids.size() : vkids.size()};
+    const int rc = kind == kVariantChess ? chess_move_root(j.batches[i], c.root, kids)
+                                         : variant_move_root(kind, j.batches[i], c.root, vkids);
+    if (rc) {
+      j.rc[i] = rc;
+      if (kind == kVariantChess) kids.resize(c.first);
+      else vkids.resize(c.first);
       continue;
-    }
-    bool ok = true;
-    std::string tok;
-    for (const char* p = a.moves ? a.moves : "";; ++p) {
-      if (*p && *p != ' ' && *p != '\t' && *p != '\n' && *p != '\r') {
-        tok += *p;
-        continue;
-      }
-      if (!tok.empty()) {
-        Move m;
-        if (!parse_uci(b, tok.c_str(), m)) {
-          ok = false;
-          break;
-        }
-        b.do_move(m);
-        tok.clear();
-      }
-      if (!*p) break;
-    }
-    if (!ok) {
-      j.rc[i] = FNNUE_E_MOVE;
-      continue;
-    }
-    std::vector<Move> ms;
-    b.legal_moves(ms);
-    if (ms.empty()) {  // mate / stalemate: nothing to play
-      j.rc[i] = FNNUE_E_MOVE;
-      continue;
-    }
-    Cand c{i, {}, kids.size()};
-    for (const Move& m : ms) {
-      Board k = b;
-      k.do_move(m);
-      kids.push_back(k.pack());
-      c.uci.push_back(b.uci(m, b.chess960));
     }
     cands.push_back(std::move(c));
   }
-  if (kids.empty()) return FNNUE_OK;
-  std::vector<int32_t> ps(kids.size()), po(kids.size());
-  if (int rc = fnnue_eval_positions(ctx, kids.data(), kids.size(), ps.data(), po.data())) return rc;
+  const size_t nk = kind == kVariantChess ? kids.size() : vkids.size();
+  std::vector<int32_t> ps(nk), po(nk);
+  if (nk) {
+    const int rc = kind == kVariantChess ? fnnue_eval_positions(ctx[kind], kids.data(), nk, ps.data(), po.data())
+                                         : fnnue_eval_vpositions(ctx[kind], vkids.data(), nk, ps.data(), po.data());
+    if (rc) return rc;
+  }
   for (const Cand& c : cands) {
     fnnue_position_response& r = j.out[j.off[c.batch]];
+    if (c.root.uci.empty()) {
+      terminal_response(r, c.root.fin);
+      continue;
+    }
+    // rank: 2 = mates, 1 = evaluated, 0 = never (value orders within a rank)
     size_t best = 0;
+    int best_rank = -1;
     int64_t bv = INT64_MIN;
-    for (size_t k = 0; k < c.uci.size(); ++k) {
+    for (size_t k = 0; k < c.root.uci.size(); ++k) {
       const size_t x = c.first + k;
-      const int64_t v = -(((int64_t)ps[x] + po[x]) / 16);  // Stockfish value of the child, negated
-      if (v > bv) {
+      const uint8_t f = c.root.kid_fin[k];
+      int rank = 1;
+      int64_t v;
+      if (f & (kFinalCheck | kFinalExtinct) && (f & kFinalNoMoves)) {
+        rank = 2;
+        v = 0;
+      } else if (f & kFinalNoMoves) {
+        v = 0;  // stalemate
+      } else {
+        v = -(((int64_t)ps[x] + po[x]) / 16);  // Stockfish value of the child, negated
+      }
+      if (rank > best_rank || (rank == best_rank && v > bv)) {
+        best_rank = rank;
         bv = v;
         best = k;
       }
@@ -300,11 +416,16 @@ int fnnue_backend::moves(Job& j, const std::vector<size_t>& games) {
     const size_t x = c.first + best;
     r.psqt = -ps[x];
     r.positional = -po[x];
-    r.score_kind = FNNUE_SCORE_CP;
-    r.score = bv * 100 / norm;
     r.depth = 1;
-    r.nodes = c.uci.size();
-    std::strncpy(r.best_move, c.uci[best].c_str(), sizeof(r.best_move) - 1);
+    r.nodes = c.root.uci.size();
+    if (best_rank == 2) {
+      r.score_kind = FNNUE_SCORE_MATE;
+      r.score = 1;
+    } else {
+      r.score_kind = FNNUE_SCORE_CP;
+      r.score = bv * 100 / norm;
+    }
+    std::strncpy(r.best_move, c.root.uci[best].c_str(), sizeof(r.best_move) - 1);
   }
   return FNNUE_OK;
 }
@@ -325,18 +446,19 @@ void fnnue_backend::run(Job& j) {
     j.err = g_err;
     return;
   }
-  std::vector<size_t> ana, mov;
+  std::vector<size_t> ana[kKinds], mov[kKinds];
   std::vector<uint8_t> skip(j.off[nb], 0);
   for (size_t i = 0; i < nb; ++i) {
     const fnnue_acquired& a = j.batches[i];
     if (j.rc[i]) continue;
-    if (!chess_variant(a.variant) || a.multipv < 0) {  // Fairy-Stockfish (routed by flavour): not this backend
-      j.rc[i] = FNNUE_E_ARG;
+    const int kind = kind_of(a.variant);
+    if (kind < 0 || !ctx[kind] || a.multipv < 0) {  // no net for this variant on this backend
+      j.rc[i] = kind < 0 || !ctx[kind] ? FNNUE_E_ARCH : FNNUE_E_ARG;
       continue;
     }
     const uint32_t n = j.off[i + 1] - j.off[i];
     if (a.work == FNNUE_WORK_MOVE) {
-      mov.push_back(i);
+      mov[kind].push_back(i);
       continue;
     }
     uint32_t live = n;
@@ -345,12 +467,14 @@ void fnnue_backend::run(Job& j) {
         skip[j.off[i] + a.skip_positions[k]] = 1;
         --live;
       }
-    if (live) ana.push_back(i);  // all skipped: completed without the engine (IncomingError::AllSkipped)
+    if (live) ana[kind].push_back(i);  // all skipped: completed without the engine (IncomingError::AllSkipped)
   }
   std::memset(j.out, 0, j.off[nb] * sizeof(fnnue_position_response));
-  std::vector<size_t> base(nb, 0);
-  int rc = analysis(j, ana, base);
-  if (rc == FNNUE_OK) rc = moves(j, mov);
+  int rc = FNNUE_OK;
+  for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k) {
+    if (!ana[k].empty()) rc = analysis(j, k, ana[k], skip);
+    if (rc == FNNUE_OK && !mov[k].empty()) rc = moves(j, k, mov[k]);
+  }
   if (rc) {
     j.ret = rc;
     j.err = g_err;
@@ -360,35 +484,18 @@ void fnnue_backend::run(Job& j) {
   uint64_t nodes = 0;
   for (size_t i = 0; i < nb; ++i) {
     if (j.rc[i]) continue;
-    if (j.batches[i].work == FNNUE_WORK_MOVE) {
-      nodes += j.out[j.off[i]].nodes;
-      continue;
-    }
-    for (uint32_t k = j.off[i]; k < j.off[i + 1]; ++k) nodes += skip[k] ? 0 : 1;
+    for (uint32_t k = j.off[i]; k < j.off[i + 1]; ++k) nodes += j.out[k].nodes;
   }
   const uint64_t ms = (uint64_t)(sec * 1e3);
   const uint32_t nps = sec > 0 ? (uint32_t)std::min(4.0e9, (double)nodes / sec) : 0;
   for (size_t i = 0; i < nb; ++i) {
     if (j.rc[i]) continue;
-    const bool is_move = j.batches[i].work == FNNUE_WORK_MOVE;
     for (uint32_t k = j.off[i]; k < j.off[i + 1]; ++k) {
       fnnue_position_response& r = j.out[k];
       r.position_id = k - j.off[i];
       r.time_ms = ms;
       r.nps = nps;
-      if (is_move) continue;  // filled by moves()
-      if (skip[k]) {
-        r.skipped = 1;
-        continue;
-      }
-      const size_t x = base[i] + r.position_id;
-      r.matrix = j.batches[i].multipv > 0 ? 1 : 0;  // Work::matrix_wanted: multipv is Some
-      r.psqt = hpsqt[x];
-      r.positional = hpositional[x];
-      r.score_kind = FNNUE_SCORE_CP;
-      r.score = to_cp(r.psqt, r.positional, norm);
-      r.depth = 0;
-      r.nodes = 1;
+      if (skip[k]) r.skipped = 1;
     }
   }
   j.ret = FNNUE_OK;
@@ -409,12 +516,19 @@ int fnnue_backend_batch_size(const fnnue_acquired* a, size_t* n) {
   return FNNUE_OK;
 }
 
-int fnnue_backend_channel(const fnnue_net* net, int device, const fnnue_backend_init* init, fnnue_backend** out) {
-  if (!net || !out) return fail(FNNUE_E_ARG, "null argument");
+int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const fnnue_backend_init* init,
+                               fnnue_backend** out) {
+  if (!nets || !out) return fail(FNNUE_E_ARG, "null argument");
   *out = nullptr;
-  int variant = 0;
-  if (int rc = fnnue_net_variant(net, &variant)) return rc;
-  if (variant != 0) return fail(FNNUE_E_ARCH, "the backend evaluates standard chess: a chess (HalfKAv2_hm) net");
+  const fnnue_net* slot[kKinds] = {nets->chess, nets->crazyhouse, nets->atomic};
+  if (!slot[0] && !slot[1] && !slot[2]) return fail(FNNUE_E_ARG, "no net");
+  static const char* const kName[kKinds] = {"chess (HalfKAv2_hm)", "crazyhouse", "atomic"};
+  for (int k = 0; k < kKinds; ++k) {
+    if (!slot[k]) continue;
+    int variant = -1;
+    if (int rc = fnnue_net_variant(slot[k], &variant)) return rc;
+    if (variant != k) return fail(FNNUE_E_ARCH, std::string("the ") + kName[k] + " slot needs a " + kName[k] + " net");
+  }
   if (init && init->normalize_to_pawn < 0) return fail(FNNUE_E_ARG, "normalize_to_pawn must be positive");
   fnnue_backend* b = nullptr;
   try {
@@ -422,23 +536,39 @@ int fnnue_backend_channel(const fnnue_net* net, int device, const fnnue_backend_
   } catch (const std::bad_alloc&) {
     return fail(FNNUE_E_OOM, "host allocation failed");
   }
+  b->device = device;
   if (init && init->normalize_to_pawn > 0) b->norm = init->normalize_to_pawn;
-  if (int rc = fnnue_ctx_create(net, device, &b->ctx)) {
-    delete b;
-    return rc;
+  for (int k = 0; k < kKinds; ++k) {
+    if (!slot[k]) continue;
+    if (int rc = fnnue_ctx_create(slot[k], device, &b->ctx[k])) {
+      for (fnnue_ctx* c : b->ctx) fnnue_ctx_free(c);
+      delete b;
+      return rc;
+    }
   }
   try {
     b->th = std::thread([b] {
-      DeviceGuard g(b->ctx->device);
+      DeviceGuard g(b->device);
       b->loop();
     });
   } catch (const std::system_error&) {
-    fnnue_ctx_free(b->ctx);
+    for (fnnue_ctx* c : b->ctx) fnnue_ctx_free(c);
     delete b;
     return fail(FNNUE_E_OOM, "could not start the actor thread");
   }
   *out = b;
   return FNNUE_OK;
+}
+
+int fnnue_backend_channel(const fnnue_net* net, int device, const fnnue_backend_init* init, fnnue_backend** out) {
+  if (!net || !out) return fail(FNNUE_E_ARG, "null argument");
+  int variant = 0;
+  if (int rc = fnnue_net_variant(net, &variant)) return rc;
+  fnnue_backend_nets nets{};
+  if (variant == kVariantChess) nets.chess = net;
+  else if (variant == kVariantCrazyhouse) nets.crazyhouse = net;
+  else nets.atomic = net;
+  return fnnue_backend_channel_nets(&nets, device, init, out);
 }
 
 void fnnue_backend_free(fnnue_backend* b) {
@@ -450,10 +580,11 @@ void fnnue_backend_free(fnnue_backend* b) {
   b->cv.notify_all();
   if (b->th.joinable()) b->th.join();
   {
-    DeviceGuard g(b->ctx->device);
-    for (DevBuf* d : {&b->text, &b->fen_off, &b->mv_off, &b->pos, &b->goff, &b->psqt, &b->positional}) d->release();
+    DeviceGuard g(b->device);
+    for (DevBuf* d : {&b->text, &b->fen_off, &b->mv_off, &b->pos, &b->goff, &b->psqt, &b->positional, &b->fin})
+      d->release();
   }
-  fnnue_ctx_free(b->ctx);
+  for (fnnue_ctx* c : b->ctx) fnnue_ctx_free(c);
   delete b;
 }
 

@@ -30,6 +30,13 @@ DBoard to_dboard(const Board& b);
 
 constexpr uint32_t kBuildErrFen = 1, kBuildErrMove = 2;
 
+// State of a game's last position (optional builder output, one byte per
+// game): a game that ended on the board ends there, since no move can follow.
+// The engine answers such a root with `bestmove (none)` and `score mate 0`
+// (checkmated, or atomic: its king exploded) or `score cp 0` (stalemate)
+// ([ref] src/stockfish.rs:359-376 parses them to Score::Mate(0) / Cp(0)).
+constexpr uint8_t kFinalNoMoves = 1, kFinalCheck = 2, kFinalExtinct = 4;
+
 struct BuildResult {
   hipError_t hip = hipSuccess;
   bool capacity = false;   // outputs too small: n_out / n_groups say what is needed
@@ -40,10 +47,12 @@ struct BuildResult {
 // text: game g's FEN in [fen_off[g], mv_off[g]), its space-separated UCI moves
 // in [mv_off[g], fen_off[g + 1]).  children = false: every ply of every game,
 // group g = game g; children = true: one group per ply = the ply's position
-// followed by its legal children (Board::legal_moves order).  Synchronises `s`.
+// followed by its legal children (Board::legal_moves order).  d_final
+// (optional, ngames bytes): kFinal* flags of each game's last position.
+// Synchronises `s`.
 BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
-                               size_t off_cap, hipStream_t s);
+                               size_t off_cap, hipStream_t s, uint8_t* d_final = nullptr);
 
 // Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub); synchronises s.
 hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s);
@@ -52,7 +61,7 @@ hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n
 // crazyhouse / atomic FENs and UCI moves (drops "P@e4"), fnnue_vpos records.
 BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                 uint32_t ngames, bool children, fnnue_vpos* d_out, size_t cap, uint32_t* d_group_off,
-                                size_t off_cap, hipStream_t s);
+                                size_t off_cap, hipStream_t s, uint8_t* d_final = nullptr);
 
 // Leaf count of perft(depth) summed over the frontier boards (1 <= depth <= 3).
 hipError_t perft_device(const std::vector<DBoard>& frontier, int depth, uint64_t* nodes);

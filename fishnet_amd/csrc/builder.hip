@@ -408,7 +408,7 @@ __device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t gam
 __global__ void replay_kernel(const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
                               const uint32_t* __restrict__ mv_off, uint32_t ngames,
                               const uint32_t* __restrict__ ply_off, fnnue_pos* __restrict__ out,
-                              DBoard* __restrict__ states, uint32_t* __restrict__ err) {
+                              DBoard* __restrict__ states, uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngames) return;
   DBoard b;
@@ -434,6 +434,16 @@ __global__ void replay_kernel(const char* __restrict__ text, const uint32_t* __r
     ++o;
     if (out) out[o] = pack(b);
     if (states) states[o] = b;
+  }
+  if (final) {
+    bool any = false;
+    for_each_legal(b, [&](const DMove&) -> bool {
+      any = true;
+      return false;
+    });
+    const int k = king_sq(b, b.stm);
+    const bool check = k >= 0 && attacked(b, k, b.stm ^ 1, b.bc[0] | b.bc[1]);
+    final[g] = (uint8_t)((any ? 0 : kFinalNoMoves) | (check ? kFinalCheck : 0));
   }
 }
 
@@ -517,7 +527,7 @@ DBoard to_dboard(const Board& h) {
 
 BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
-                               size_t off_cap, hipStream_t s) {
+                               size_t off_cap, hipStream_t s, uint8_t* d_final) {
   BuildResult R;
   auto fail = [&](hipError_t e) {
     R.hip = e;
@@ -557,7 +567,7 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
       return R;
     }
     hipLaunchKernelGGL(replay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
-                       ngames, ply_off, d_out, (DBoard*)nullptr, err);
+                       ngames, ply_off, d_out, (DBoard*)nullptr, err, d_final);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
     if ((e = hipMemcpyAsync(d_group_off, ply_off, (size_t)(ngames + 1) * 4, hipMemcpyDeviceToDevice, s)) !=
         hipSuccess)
@@ -567,7 +577,7 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
     if ((e = alloc((void**)&cnt, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
     if ((e = alloc((void**)&coff, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
     hipLaunchKernelGGL(replay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
-                       ngames, ply_off, (fnnue_pos*)nullptr, states, err);
+                       ngames, ply_off, (fnnue_pos*)nullptr, states, err, d_final);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
     uint32_t herr[4];
     if ((e = hipMemcpyAsync(herr, err, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);

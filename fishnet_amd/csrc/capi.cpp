@@ -194,6 +194,35 @@ bool valid_host_pos(const fnnue_pos& p) {
   return wk == 1 && bk == 1 && n <= 32 && p.stm <= 1;
 }
 
+int host_vpos_state(const fnnue_vpos& p, int variant) {
+  int n = 0, wk = 0, bk = 0;
+  for (int s = 0; s < 64; ++s) {
+    const int pc = (p.sq[s >> 1] >> (4 * (s & 1))) & 15;
+    if (!pc) continue;
+    if (pc == 7 || pc == 8 || pc == 15) return 0;
+    ++n;
+    wk += pc == 6;
+    bk += pc == 14;
+  }
+  for (int i = 0; i < 10; ++i) {
+    if (p.hand[i] > kVHandSlots || (variant != kVariantCrazyhouse && p.hand[i])) return 0;
+    n += p.hand[i];
+  }
+  if (n > 32 || p.stm > 1) return 0;
+  if (variant == kVariantAtomic && wk + bk == 1) return 2;
+  return wk == 1 && bk == 1 ? 1 : 0;
+}
+
+int name_invalid_v(int rc, const fnnue_vpos* pos, size_t n, int variant, size_t base) {
+  if (rc != FNNUE_E_POSITION) return rc;
+  for (size_t i = 0; i < n; ++i)
+    if (!host_vpos_state(pos[i], variant))
+      return fail(FNNUE_E_POSITION, "invalid variant position at index " + std::to_string(base + i) +
+                                        " (one king per side, or atomic with one king exploded; <= 32 pieces on "
+                                        "board and in hand, <= 16 of a type in hand, valid piece codes, stm 0/1)");
+  return rc;
+}
+
 // After the device latched FNNUE_E_POSITION: the message names the first
 // invalid position (the host rule is the device's, valid_host_pos).
 int name_invalid(int rc, const fnnue_pos* pos, size_t n) {
@@ -778,9 +807,7 @@ int fnnue_eval_vpositions(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t n, int32
     HIP_TRY(hipMemcpyAsync(psqt + b, ctx->d_psqt, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
     HIP_TRY(hipMemcpyAsync(positional + b, ctx->d_positional, m * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
     HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-    if ((rc = latched(ctx)) == FNNUE_E_POSITION) return fail(rc, "invalid variant position in positions " +
-                                                               std::to_string(b) + ".." + std::to_string(b + m));
-    if (rc) return rc;
+    if ((rc = latched(ctx))) return name_invalid_v(rc, pos + b, m, ctx->variant, b);
   }
   return FNNUE_OK;
 }
@@ -870,8 +897,7 @@ int fnnue_eval_vgroups(fnnue_ctx* ctx, const fnnue_vpos* pos, size_t npos, const
   HIP_TRY(hipMemcpyAsync(psqt, ctx->d_psqt, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
   HIP_TRY(hipMemcpyAsync(positional, ctx->d_positional, npos * 4, hipMemcpyDeviceToHost, ctx->stream), "D2H");
   HIP_TRY(hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-  if ((rc = latched(ctx)) == FNNUE_E_POSITION) return fail(rc, "invalid variant position in the batch");
-  return rc;
+  return name_invalid_v(latched(ctx), pos, npos, ctx->variant, 0);
 }
 
 // ---- batch building ----
@@ -900,6 +926,31 @@ int split_moves(const char* moves, std::vector<std::string>& out) {
   return FNNUE_OK;
 }
 }  // namespace
+}  // extern "C"
+
+namespace fnnue::detail {
+
+int game_end_chess(const char* fen, const char* moves, int* flags) {
+  Board b;
+  std::string err;
+  if (!board_from_fen(fen, b, &err)) return fail(FNNUE_E_FEN, err);
+  std::vector<std::string> ms;
+  split_moves(moves, ms);
+  for (size_t i = 0; i < ms.size(); ++i) {
+    Move m;
+    if (!parse_uci(b, ms[i].c_str(), m))
+      return fail(FNNUE_E_MOVE, "illegal move " + ms[i] + " at ply " + std::to_string(i + 1) + " in " + b.fen());
+    b.do_move(m);
+  }
+  std::vector<Move> legal;
+  b.legal_moves(legal);
+  *flags = (legal.empty() ? FNNUE_END_NO_MOVES : 0) | (b.in_check() ? FNNUE_END_CHECK : 0);
+  return FNNUE_OK;
+}
+
+}  // namespace fnnue::detail
+
+extern "C" {
 
 int fnnue_game_positions(const char* fen, const char* moves, fnnue_pos* out, size_t cap, size_t* n_out) {
   if (!fen || !n_out) return fail(FNNUE_E_ARG, "null argument");

@@ -76,6 +76,7 @@ struct ChessFs {
     uint32_t hand[10];
     int nfeat;
     bool ok;
+    bool over;  // never for chess (variant_common.h: atomic game over)
   };
   template <bool kOcc = true>
   __device__ static __forceinline__ Dec decode(const Pos* p) {
@@ -83,6 +84,7 @@ struct ChessFs {
     d.b = lane_decode<kOcc>(p);
     d.nfeat = d.b.cnt;
     d.ok = d.b.ok;
+    d.over = false;
     return d;
   }
   // The base of a delta: its board words, with validity and king squares
@@ -216,7 +218,7 @@ __device__ __forceinline__ void seg_delta_one(const typename Fs::Pos* __restrict
     bucket[i] = 0xFF;
     ref[i] = ref[n + i] = 1;
     r0 = r1 = 1;
-    atomicOr(err, 1u);
+    if (!B.over) atomicOr(err, 1u);  // an exploded king (atomic) is a result (0, 0), not an error
     return;
   }
   const uint32_t bk = (uint32_t)(B.b.cnt - 1) >> 2;  // board pieces
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(256) void seg_delta_kernel(const typename Fs::Pos* 
     for (uint32_t k = threadIdx.x; k < ctr_words; k += blockDim.x) ctr[k] = 0;
   const uint32_t i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
   typename Fs::Dec B;
-  B.ok = false;
+  B.ok = B.over = false;
   B.b.wk = B.b.bk = 0;
   if (i < n) B = Fs::template decode<false>(pos + i);
   info[threadIdx.x] = seg_info(B);

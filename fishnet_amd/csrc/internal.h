@@ -97,5 +97,11 @@ int latched(fnnue_ctx* c);
 bool valid_host_pos(const fnnue_pos& p);
 // After FNNUE_E_POSITION latched: names the first invalid position.
 int name_invalid(int rc, const fnnue_pos* pos, size_t n);
+// A variant position as the device sees it: 0 invalid, 1 evaluated, 2 atomic
+// game over (one king exploded: result (0, 0), not an error).
+int host_vpos_state(const fnnue_vpos& p, int variant);
+int name_invalid_v(int rc, const fnnue_vpos* pos, size_t n, int variant, size_t base);
+// fnnue_game_end for standard chess (board.cpp rules).
+int game_end_chess(const char* fen, const char* moves, int* flags);
 
 }  // namespace fnnue::detail

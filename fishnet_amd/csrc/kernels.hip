@@ -469,8 +469,12 @@ __global__ __launch_bounds__(64 * W0Lds<HD>::kWaves) void stack_kernel(
       for (int j = 0; j < KP; ++j) {  // in place: LDS ops of one wave complete in order
         st[wr * 8 + (wc ^ (wr & 7))] = a[2 * j];
         st[(wr + 8) * 8 + (wc ^ (wr & 7))] = a[2 * j + 1];
+        // other lanes' stores are read back: keep the compiler from reordering
+        // across the exchange (no instruction: the hardware keeps the order)
+        wave_lds_sync();
         a[2 * j] = st[r16 * 8 + (g ^ (r16 & 7))];
         a[2 * j + 1] = st[r16 * 8 + ((4 + g) ^ (r16 & 7))];
+        wave_lds_sync();  // this step's reads before the next step's stores
       }
     } else {
       const v4i* xr = reinterpret_cast<const v4i*>(x + (size_t)(row_ok ? prow : p0) * HD);

@@ -90,7 +90,9 @@ struct LaneBoard {
   uint32_t w[8];
   uint64_t occ;
   int stm, wk, bk, cnt;
-  bool ok;
+  int nwk, nbk;  // kings of each colour (an atomic game ends with one exploded)
+  bool sane;     // valid piece codes, <= 32 pieces, stm 0 / 1 (kings not counted)
+  bool ok;       // sane and one king per side
 };
 
 // Bit 4k+3 set iff nibble k of y is zero.
@@ -133,7 +135,10 @@ __device__ __forceinline__ LaneBoard lane_decode(const fnnue_pos* p) {
     bad |= (w & (w >> 1) & (w >> 2) & 0x11111111u) | zero_nibbles(w ^ 0x88888888u);
   }
   b.cnt = cnt;
-  b.ok = !bad && nwk == 1 && nbk == 1 && b.cnt <= 32 && b.stm <= 1;
+  b.nwk = nwk;
+  b.nbk = nbk;
+  b.sane = !bad && b.cnt <= 32 && b.stm <= 1;
+  b.ok = b.sane && nwk == 1 && nbk == 1;
   return b;
 }
 

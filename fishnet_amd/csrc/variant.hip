@@ -33,7 +33,7 @@ __global__ __launch_bounds__(1024) void vplan_count_kernel(const fnnue_vpos* __r
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
     const VariantBoard v = vdecode<false>(pos + p, pockets != 0);  // counts only: no occupancy mask
     if (!v.ok) {
-      bad = 1;
+      bad |= v.over ? 0u : 1u;  // an exploded king is a result (0, 0), not an error
       atomicAdd(&h[kVItemBins + 8], 1u);
     } else {
       atomicAdd(&h[vblock(0, v.b.wk) * 33 + v.nfeat], 1u);

@@ -14,6 +14,7 @@ struct VariantBoard {
   uint32_t hand[10];  // white P N B R Q, black P N B R Q
   int nfeat;          // pieces on board + in hand (= list length + 1 per perspective)
   bool ok;
+  bool over;          // atomic game over: one king exploded (no NNUE eval, not an error)
 };
 
 template <bool kOcc = true>
@@ -32,6 +33,11 @@ __device__ __forceinline__ VariantBoard vdecode(const fnnue_vpos* p, bool pocket
   v.b.stm = reinterpret_cast<const uint8_t*>(p)[32];
   v.nfeat = v.b.cnt + tot;
   v.ok = v.b.ok && v.b.stm <= 1 && !bad && v.nfeat <= 32;
+  // Atomic: a capture next to a king explodes it and ends the game; the
+  // position after it (exactly one king left) is a terminal record the
+  // evaluator answers with (0, 0) without latching an error.  Only variants
+  // without pockets here (crazyhouse kings are never removed).
+  v.over = !pockets && v.b.sane && !bad && v.nfeat <= 32 && v.b.nwk + v.b.nbk == 1;
   return v;
 }
 

@@ -133,18 +133,6 @@ int pack_checked(const vb::VBoard& b, fnnue_vpos* out) {
   return FNNUE_OK;
 }
 
-std::string square_name(int s) { return std::string{(char)('a' + (s & 7)), (char)('1' + (s >> 3))}; }
-
-// UCI text of a legal move: drops "N@f3", castling king-takes-rook in Chess960
-// positions and the king's two-square step otherwise, promotions "e7e8q".
-std::string vuci(const vb::VBoard& b, const vb::VMove& m) {
-  if (m.kind == 2) return std::string(1, "PNBRQ"[m.piece - 1]) + "@" + square_name(m.to);
-  int to = m.to;
-  if (m.kind == 1 && !b.c960) to = (m.from & 56) + (m.to > m.from ? 6 : 2);
-  std::string u = square_name(m.from) + square_name(to);
-  if (m.kind == 0 && m.piece) u += "nbrq"[m.piece - 2];
-  return u;
-}
 
 bool valid_variant(int variant) { return variant == FNNUE_VARIANT_CRAZYHOUSE || variant == FNNUE_VARIANT_ATOMIC; }
 
@@ -277,6 +265,21 @@ int fnnue_game_vchildren(int variant, const char* fen, const char* moves, fnnue_
   return FNNUE_OK;
 }
 
+int fnnue_game_end(int variant, const char* fen, const char* moves, int* flags) {
+  if (!fen || !flags) return fail(FNNUE_E_ARG, "null argument");
+  *flags = 0;
+  if (variant == FNNUE_VARIANT_CHESS) return game_end_chess(fen, moves, flags);
+  if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
+  vb::VBoard last{};
+  const int rc = vreplay(variant, fen, moves, [&](const vb::VBoard& b) {
+    last = b;
+    return (int)FNNUE_OK;
+  });
+  if (rc) return rc;
+  *flags = vb::final_state(last);
+  return FNNUE_OK;
+}
+
 int fnnue_vperft(int variant, const char* fen, int depth, uint64_t* nodes) {
   if (!fen || !nodes || depth < 0) return fail(FNNUE_E_ARG, "bad argument");
   if (!valid_variant(variant)) return fail(FNNUE_E_ARG, "unknown variant " + std::to_string(variant));
@@ -305,7 +308,7 @@ int fnnue_random_vgame(uint64_t seed, int variant, const char* fen, uint32_t pli
     if (legal.empty()) break;
     const vb::VMove m = legal[splitmix64(st) % legal.size()];
     if (!out.empty()) out += ' ';
-    out += vuci(b, m);
+    out += vb::vuci(b, m);
     vb::do_move(b, m);
   }
   *len = out.size();
@@ -326,7 +329,8 @@ int fnnue_random_vgames(uint64_t seed, int variant, size_t count, uint32_t max_p
   vb::parse_fen(start, 0, (uint32_t)std::strlen(start), variant, root);
   // Game i: L ~ U[0, max_plies] uniformly random legal moves from (seed, i),
   // stopping when no move is left or a king exploded (that last position is
-  // dropped: it has no king to evaluate).  Independent of the thread count.
+  // kept: an atomic game's final ply, which the evaluator answers with (0, 0)
+  // and the backend with mate 0).  Independent of the thread count.
   struct Part {
     std::vector<fnnue_vpos> pos;
     std::vector<uint32_t> sizes;
@@ -350,8 +354,8 @@ int fnnue_random_vgames(uint64_t seed, int variant, size_t count, uint32_t max_p
         });
         if (legal.empty()) break;
         vb::do_move(v, legal[splitmix64(st) % legal.size()]);
-        if (vb::king_sq(v, 0) < 0 || vb::king_sq(v, 1) < 0) break;
         P.pos.push_back(vb::pack(v));
+        if (vb::king_sq(v, 0) < 0 || vb::king_sq(v, 1) < 0) break;
       }
       P.sizes.push_back((uint32_t)(P.pos.size() - before));
     }

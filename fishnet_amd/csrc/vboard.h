@@ -26,6 +26,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <string>
 
 #include "../../include/fnnue.h"
 
@@ -305,6 +306,19 @@ __host__ __device__ void for_each_legal(const VBoard& b, F&& f, uint64_t from_ma
   }
 }
 
+// Game-end flags of a position (builder.h kFinal*): no legal move (bit 0),
+// the side to move's king attacked (bit 1), its king exploded (bit 2, atomic).
+FNNUE_HD uint8_t final_state(const VBoard& b) {
+  bool any = false;
+  for_each_legal(b, [&](const VMove&) -> bool {
+    any = true;
+    return false;
+  });
+  const int us = b.stm, k = king_sq(b, us);
+  const bool check = k >= 0 && king_danger(b, k, us, occupied(b));
+  return (uint8_t)((any ? 0 : 1) | (check ? 2 : 0) | (k < 0 ? 4 : 0));
+}
+
 FNNUE_HD fnnue_vpos pack(const VBoard& b) {
   fnnue_vpos p;
   uint32_t w[8];
@@ -502,6 +516,19 @@ FNNUE_HD bool match_uci(const VBoard& b, const char* tok, int len, VMove& out) {
 }
 
 #undef FNNUE_HD
+
+// UCI text of a legal move (host): drops "N@f3", castling king-takes-rook in
+// Chess960 positions and the king's two-square step otherwise, promotions
+// "e7e8q".
+inline std::string vuci(const VBoard& b, const VMove& m) {
+  auto sq = [](int s) { return std::string{(char)('a' + (s & 7)), (char)('1' + (s >> 3))}; };
+  if (m.kind == 2) return std::string(1, "PNBRQ"[m.piece - 1]) + "@" + sq(m.to);
+  int to = m.to;
+  if (m.kind == 1 && !b.c960) to = (m.from & 56) + (m.to > m.from ? 6 : 2);
+  std::string u = sq(m.from) + sq(to);
+  if (m.kind == 0 && m.piece) u += "nbrq"[m.piece - 2];
+  return u;
+}
 
 }  // namespace vb
 }  // namespace fnnue

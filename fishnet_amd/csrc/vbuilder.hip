@@ -41,7 +41,8 @@ __device__ __forceinline__ void vlatch(uint32_t* err, uint32_t code, uint32_t ga
 __global__ void vreplay_kernel(int variant, const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
                                const uint32_t* __restrict__ mv_off, uint32_t ngames,
                                const uint32_t* __restrict__ ply_off, fnnue_vpos* __restrict__ out,
-                               vb::VBoard* __restrict__ states, uint32_t* __restrict__ err) {
+                               vb::VBoard* __restrict__ states, uint32_t* __restrict__ err,
+                               uint8_t* __restrict__ final) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngames) return;
   vb::VBoard b;
@@ -67,6 +68,7 @@ __global__ void vreplay_kernel(int variant, const char* __restrict__ text, const
     if (out) out[o] = vb::pack(b);
     if (states) states[o] = b;
   }
+  if (final) final[g] = vb::final_state(b);
 }
 
 __global__ void vcount_children_kernel(const vb::VBoard* __restrict__ states, uint32_t n, uint32_t* __restrict__ cnt) {
@@ -100,7 +102,7 @@ __global__ void vwrite_children_kernel(const vb::VBoard* __restrict__ states, ui
 
 BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                 uint32_t ngames, bool children, fnnue_vpos* d_out, size_t cap, uint32_t* d_group_off,
-                                size_t off_cap, hipStream_t s) {
+                                size_t off_cap, hipStream_t s, uint8_t* d_final) {
   BuildResult R;
   auto fail = [&](hipError_t e) {
     R.hip = e;
@@ -140,7 +142,7 @@ BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t*
       return R;
     }
     hipLaunchKernelGGL(vreplay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, variant, d_text, d_fen_off,
-                       d_mv_off, ngames, ply_off, d_out, (vb::VBoard*)nullptr, err);
+                       d_mv_off, ngames, ply_off, d_out, (vb::VBoard*)nullptr, err, d_final);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
     if ((e = hipMemcpyAsync(d_group_off, ply_off, (size_t)(ngames + 1) * 4, hipMemcpyDeviceToDevice, s)) !=
         hipSuccess)
@@ -150,7 +152,7 @@ BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t*
     if ((e = alloc((void**)&cnt, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
     if ((e = alloc((void**)&coff, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
     hipLaunchKernelGGL(vreplay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, variant, d_text, d_fen_off,
-                       d_mv_off, ngames, ply_off, (fnnue_vpos*)nullptr, states, err);
+                       d_mv_off, ngames, ply_off, (fnnue_vpos*)nullptr, states, err, d_final);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
     uint32_t herr[4];
     if ((e = hipMemcpyAsync(herr, err, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);

@@ -168,6 +168,19 @@ def game_vchildren(variant: int, fen: str, moves: str | list[str]) -> tuple[np.n
     return out[: n.value], off[: g.value + 1]
 
 
+END_NO_MOVES, END_CHECK, END_EXTINCT = 1, 2, 4
+
+
+def game_end(fen: str, moves: str | list[str] = "", variant: int = 0) -> int:
+    """FNNUE_END_* flags of the position after `moves` (host replay): no legal
+    move, side to move in check, its king exploded (atomic)."""
+    if not isinstance(moves, str):
+        moves = " ".join(moves)
+    flags = C.c_int()
+    N.check(N.lib.fnnue_game_end(variant, fen.encode(), moves.encode(), C.byref(flags)))
+    return flags.value
+
+
 def vperft(variant: int, fen: str, depth: int) -> int:
     nodes = C.c_uint64()
     N.check(N.lib.fnnue_vperft(variant, fen.encode(), depth, C.byref(nodes)))

@@ -155,7 +155,8 @@ int fnnue_random_vgame(uint64_t seed, int variant, const char *fen, uint32_t pli
 /* Test / bench inputs: every ply of `count` seeded random LEGAL games of the
  * variant from its start position (L ~ U[0, max_plies] plies, drops included),
  * as CHAIN groups; a game ends early with no legal move or an exploded king
- * (that position is not emitted).  Deterministic for (seed, index). */
+ * (that position is the game's last: see fnnue_eval_vpositions on game-over
+ * records).  Deterministic for (seed, index). */
 int fnnue_random_vgames(uint64_t seed, int variant, size_t count, uint32_t max_plies, int threads, fnnue_vpos *out,
                         size_t cap, uint32_t *off, size_t off_cap, size_t *n_out, size_t *n_groups);
 /* The batch expansion on the device, as fnnue_build_batch[_device] (same text
@@ -170,7 +171,13 @@ int fnnue_build_vbatch(fnnue_ctx *ctx, int variant, const char *text, size_t tex
                        size_t off_cap, size_t *n_out, size_t *n_groups);
 /* Evaluation of variant positions on a context created from a variant net
  * (fnnue_ctx_create / fnnue_multi_create): the LDS-stationary feature
- * transformer over the variant tiles, then the MFMA layer stacks. */
+ * transformer over the variant tiles, then the MFMA layer stacks.
+ * Game-over records: an atomic position with exactly one king (the other
+ * exploded — how atomic games end, and every child that captures next to the
+ * enemy king) has no NNUE evaluation; its result is psqt = positional = 0 and
+ * it is not an error (the game's result is the caller's: fnnue_game_end,
+ * the backend's mate 0).  Any other position without one king per side fails
+ * the call with FNNUE_E_POSITION, the message naming its index. */
 int fnnue_eval_vpositions(fnnue_ctx *ctx, const fnnue_vpos *pos, size_t n, int32_t *psqt, int32_t *positional);
 int fnnue_eval_vpositions_device(fnnue_ctx *ctx, const fnnue_vpos *d_pos, size_t n, int32_t *d_psqt,
                                  int32_t *d_positional, void *stream);
@@ -298,6 +305,15 @@ int fnnue_game_positions(const char *fen, const char *moves, fnnue_pos *out, siz
  * out[off[g]] is ply g, followed by its children.  off has n_groups+1 entries. */
 int fnnue_game_children(const char *fen, const char *moves, fnnue_pos *out, size_t cap, uint32_t *off,
                         size_t off_cap, size_t *n_out, size_t *n_groups);
+/* Has the game ended on the board after `moves`?  *flags = FNNUE_END_*: no
+ * legal move, the side to move's king attacked, its king exploded (atomic).
+ * A position without a legal move is where the engine answers `score mate 0`
+ * (checkmate / explosion) or `score cp 0` (stalemate) with `bestmove (none)`
+ * ([ref] src/stockfish.rs:359-376).  variant: FNNUE_VARIANT_* (host replay). */
+#define FNNUE_END_NO_MOVES 1
+#define FNNUE_END_CHECK 2
+#define FNNUE_END_EXTINCT 4
+int fnnue_game_end(int variant, const char *fen, const char *moves, int *flags);
 /* Seeded random playouts from the start position (splitmix64; L ~ U[min,max]
  * plies of uniformly random legal moves, stopping at mate, stalemate or the
  * 50-move rule).  Deterministic for a given (seed, index) regardless of threads.

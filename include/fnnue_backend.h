@@ -11,17 +11,21 @@
  * 100-103, and the batch expanded by IncomingBatch::from_acquired
  * (src/queue.rs:518-627) from an AcquireResponseBody (src/api.rs:293-309).
  *
- * Here the same pair is a channel to one evaluator on one GPU: the actor is a
- * worker thread owning an fnnue_ctx; a go() sends it whole acquired batches
- * (capacity-1 channel: a second caller waits, as on the reference's
- * mpsc::channel(1)) and returns one response per position.  The expansion
- * (FEN parse, UCI replay, every ply) runs on the device (fnnue_build_batch_
- * device), the plies are evaluated incrementally along each game (CHAIN
- * groups), and the two raw NNUE terms become a Score::Cp.  A batch that fails
- * (unparsable FEN, illegal move, a variant this backend does not evaluate)
- * gets its own nonzero code in batch_rc — PositionFailed{batch_id}
- * (queue.rs:207-213 drops that batch) — while the other batches of the call
- * complete.  A nonzero return of go() itself (device failure) fails them all.
+ * Here the same pair is a channel to one evaluator per net on one GPU: the
+ * actor is a worker thread owning an fnnue_ctx per net (chess, and optionally
+ * the crazyhouse and atomic Fairy-Stockfish variant nets); a go() sends it
+ * whole acquired batches (capacity-1 channel: a second caller waits, as on
+ * the reference's mpsc::channel(1)) and returns one response per position.
+ * Each batch goes to the net of its variant (the reference picks the engine
+ * by EngineFlavor, src/queue.rs:530-539, and the variant, src/assets.rs:
+ * 384-391).  The expansion (FEN parse, UCI replay, every ply) runs on the
+ * device (fnnue_build_batch_device / fnnue_build_vbatch_device), the plies are
+ * evaluated incrementally along each game (CHAIN groups), and the two raw NNUE
+ * terms become a Score::Cp.  A batch that fails (unparsable FEN, illegal move,
+ * a variant this backend has no net for) gets its own nonzero code in
+ * batch_rc — PositionFailed{batch_id} (queue.rs:207-213 drops that batch) —
+ * while the other batches of the call complete.  A nonzero return of go()
+ * itself (device failure) fails them all.
  *
  * Score (static evaluation; search is outside this path):
  *   v  = (psqt + positional) / 16            Stockfish's NNUE value (internal
@@ -34,9 +38,18 @@
  *                                             uci.cpp; 361 in SF 15.1 as recalled,
  *                                             a parameter because it is unpinned)
  * Analysis work: one response per ply, depth 0, nodes 1, no pv / best move.
- * Move work: the root after all moves; its legal children are evaluated and
- * the move maximising -v(child) is the best move (depth 1, nodes = children,
- * score = that maximum).
+ * A position with no legal move (it can only be a game's last ply) is
+ * answered as the engine answers it — `info depth 0 score mate 0` when the
+ * side to move is checkmated (atomic: its king exploded), `score cp 0` when
+ * stalemated, `bestmove (none)` (src/stockfish.rs:359-376, 418-425): score
+ * Mate(0) / Cp(0), depth 0, nodes 0, no best move; psqt / positional still
+ * carry the NNUE terms ((0, 0) for an exploded king).
+ * Move work: the root after all moves; a one-ply search over its legal
+ * children: a child that mates (checkmate, atomic explosion of the other
+ * king) is chosen first (score Mate(1)), a stalemating child is worth 0, every
+ * other child -v(child) from its NNUE evaluation; the first maximum is the
+ * best move (depth 1, nodes = children).  A root with no legal move: no best
+ * move, Mate(0) / Cp(0), depth 0, nodes 0.
  */
 #ifndef FNNUE_BACKEND_H
 #define FNNUE_BACKEND_H
@@ -69,7 +82,8 @@ typedef struct {
                                       matrix form (AnalysisPart::Matrix, Work::matrix_wanted, api.rs:179-187)
                                       with its one line (static eval has no second PV) at depth 0 */
   const char *position;            /* root FEN (X-FEN / Shredder castling accepted) */
-  const char *variant;             /* "standard", "chess960", "fromPosition", NULL / "" = standard */
+  const char *variant;             /* "standard", "chess960", "fromPosition", NULL / "" = standard;
+                                      "crazyhouse", "atomic" (variant nets); anything else: FNNUE_E_ARCH */
   const char *moves;               /* space-separated UCI (Chess960 king-takes-rook accepted) */
   const uint32_t *skip_positions;  /* skipPositions: position ids answered as Skipped */
   size_t nskip;
@@ -91,8 +105,20 @@ typedef struct {
   char best_move[8];     /* UCI, NUL-terminated; "" for analysis */
 } fnnue_position_response;
 
-/* stockfish::channel: starts the actor (worker thread + evaluator on
- * `device`).  init may be NULL (defaults). */
+/* The nets of one backend, by the batches they evaluate.  Any may be NULL
+ * (not all); a batch whose variant has no net fails with FNNUE_E_ARCH. */
+typedef struct {
+  const fnnue_net *chess;      /* standard / chess960 / fromPosition: a HalfKAv2_hm net */
+  const fnnue_net *crazyhouse; /* a FNNUE_VARIANT_CRAZYHOUSE net (fnnue_net_load_variant) */
+  const fnnue_net *atomic;     /* a FNNUE_VARIANT_ATOMIC net */
+} fnnue_backend_nets;
+
+/* stockfish::channel: starts the actor (worker thread + one evaluator per net
+ * on `device`).  A net in the wrong slot: FNNUE_E_ARCH.  init may be NULL
+ * (defaults).  The nets may be freed after the call. */
+int fnnue_backend_channel_nets(const fnnue_backend_nets *nets, int device, const fnnue_backend_init *init,
+                               fnnue_backend **out);
+/* The one-net form: the net goes to the slot of its variant. */
 int fnnue_backend_channel(const fnnue_net *net, int device, const fnnue_backend_init *init, fnnue_backend **out);
 /* Stops the actor (after the call in flight) and frees it. */
 void fnnue_backend_free(fnnue_backend *b);

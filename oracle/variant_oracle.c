@@ -71,7 +71,9 @@ int voracle_hand_index(int variant, int persp, int color, int pt, int k, int ksq
 
 typedef struct { uint8_t board[64]; int stm; uint8_t hand[10]; int wk, bk, cnt; } ovpos;
 
-/* Unpacks and validates; returns 0 or -1. */
+/* Unpacks and validates; returns 0, -1 (invalid) or 1 (atomic game over: one
+ * king exploded — no NNUE evaluation, the result is (0, 0); fishnet's atomic
+ * games end with that position, [ref] src/queue.rs:586-600 sends every ply). */
 static int ov_unpack(int variant, const uint8_t *p, ovpos *v) {
     int nwk = 0, nbk = 0, hand_total = 0;
     v->cnt = 0;
@@ -91,7 +93,9 @@ static int ov_unpack(int variant, const uint8_t *p, ovpos *v) {
         if (v->hand[i] && variant != OV_CRAZYHOUSE) return -1;
         hand_total += v->hand[i];
     }
-    if (nwk != 1 || nbk != 1 || v->stm > 1 || v->cnt + hand_total > 32) return -1;
+    if (v->stm > 1 || v->cnt + hand_total > 32) return -1;
+    if (variant == OV_ATOMIC && nwk + nbk == 1) return 1;
+    if (nwk != 1 || nbk != 1) return -1;
     return 0;
 }
 
@@ -123,7 +127,12 @@ static void ov_refresh(const onet *n, const ovpos *v, int persp, int16_t *acc, i
 
 int voracle_eval(const onet *n, const uint8_t *p48, int32_t *psqt, int32_t *positional) {
     ovpos v;
-    if (!n->variant || ov_unpack(n->variant, p48, &v)) return -1;
+    if (!n->variant) return -1;
+    const int u = ov_unpack(n->variant, p48, &v);
+    if (u) {
+        *psqt = *positional = 0;
+        return u > 0 ? 0 : -1;
+    }
     int16_t acc[2][4096];
     int32_t psq[2][O_PSQT_BUCKETS];
     ov_refresh(n, &v, 0, acc[0], psq[0]);
@@ -153,9 +162,10 @@ int voracle_eval_groups(const onet *n, const uint8_t *packed, const uint32_t *of
         int have = 0;
         for (uint32_t i = off[g]; i < off[g + 1]; ++i) {
             ovpos v;
-            if (ov_unpack(n->variant, packed + (size_t)OV_POS_BYTES * i, &v)) {
+            const int u = ov_unpack(n->variant, packed + (size_t)OV_POS_BYTES * i, &v);
+            if (u) {
                 psqt[i] = positional[i] = 0;
-                bad = 1;
+                if (u < 0) bad = 1;
                 if (mode == 0 || i == off[g]) have = 0;
                 continue;
             }
@@ -238,6 +248,6 @@ int voracle_eval_packed(const onet *n, const uint8_t *packed, size_t count, int3
 /* Feature list of one perspective (tests: index known values, invariances). */
 int voracle_features(int variant, const uint8_t *p48, int persp, int32_t *out) {
     ovpos v;
-    if (ov_unpack(variant, p48, &v)) return -1;
+    if (ov_unpack(variant, p48, &v) != 0) return -1;
     return ov_features(variant, &v, persp, out);
 }

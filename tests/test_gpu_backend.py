@@ -1,8 +1,12 @@
 """fnnue_backend on the GPU: whole acquired batches through the actor
-(device expansion + CHAIN evaluation) against the CPU oracle on the host
-builder's positions, bit-exact; per-batch PositionFailed isolation
-([ref] src/queue.rs:207-213); move work = 1-ply argmax over the legal
-children; skipPositions; concurrent callers on the capacity-1 channel."""
+(device expansion + CHAIN evaluation) against the CPU oracles on the host
+builder's positions, bit-exact; crazyhouse / atomic batches on their variant
+nets ([ref] src/queue.rs:530-539, src/assets.rs:384-391); games that end on
+the board answered as the engine answers them (mate 0 / cp 0, no best move,
+[ref] src/stockfish.rs:359-376, 418-425); per-batch PositionFailed isolation
+([ref] src/queue.rs:207-213); move work = one-ply search over the legal
+children (mates first); skipPositions; concurrent callers on the capacity-1
+channel."""
 import json
 import os
 import threading
@@ -11,28 +15,37 @@ import numpy as np
 import pytest
 
 import fishnet_amd as F
+from fishnet_amd import _native as N
 from fishnet_amd import backend as B
-from oracle.oracle import OracleNet
+from oracle.oracle import OracleNet, VariantOracleNet
 from tests.conftest import ROOT, net_bytes
 
 pytestmark = pytest.mark.gpu
 
 GAMES = json.load(open(os.path.join(ROOT, "tests", "golden", "wcc_games.json")))["games"]
 START = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+ZH_START = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR[] w KQkq - 0 1"
 C960 = "bqnb1rkr/pp3ppp/3ppn2/2p5/5P2/P2P4/NPP1P1PP/BQ1BNRKR w HFhf - 2 9"
+ZH, AT = N.VARIANT_CRAZYHOUSE, N.VARIANT_ATOMIC
+FOOLS_MATE = "f2f3 e7e5 g2g4 d8h4"
+STALEMATE = ("7k/5Q2/5K2/8/8/8/8/8 w - - 0 1", "f6g6")
+ATOMIC_WIN = "g1f3 e7e6 f3g5 f8e7 g5f7"  # Nxf7 explodes the black king
 
 
 @pytest.fixture(scope="module")
 def chan():
     data = net_bytes(1, 1024, 0)
-    stub, actor = B.channel(F.Net.from_bytes(data), 0)
-    yield stub, OracleNet(data)
+    zh = F.synthesize_variant_net(5, 512, ZH)
+    at = F.synthesize_variant_net(6, 512, AT)
+    stub, actor = B.channel(F.Net.from_bytes(data), 0, crazyhouse=F.Net.from_bytes_variant(zh, ZH),
+                            atomic=F.Net.from_bytes_variant(at, AT))
+    yield stub, {0: OracleNet(data), ZH: VariantOracleNet(zh, ZH), AT: VariantOracleNet(at, AT)}
     actor.close()
 
 
-def expect(on, fen, moves):
-    pos = F.game_positions(fen, moves)
-    ps, po, rc = on.eval_packed(pos, threads=8)
+def expect(on, fen, moves, variant=0):
+    pos = F.game_positions(fen, moves) if variant == 0 else F.game_vpositions(variant, fen, moves)
+    ps, po, rc = on[variant].eval_packed(pos, threads=8)
     assert rc == 0
     return ps, po
 
@@ -40,6 +53,24 @@ def expect(on, fen, moves):
 def cp(ps, po, norm=361):
     v = int((int(ps) + int(po)) / 16)  # C truncation
     return int(v * 100 / norm)
+
+
+def check_rows(on, body, rows, variant=0):
+    """Every ply against the oracle; the last ply of a game that ended on the
+    board as the engine answers it."""
+    ps, po = expect(on, body.position, body.moves, variant)
+    assert [r.position_id for r in rows] == list(range(len(ps)))
+    assert [r.psqt for r in rows] == ps.tolist()
+    assert [r.positional for r in rows] == po.tolist()
+    end = F.game_end(body.position, body.moves, variant)
+    for k, r in enumerate(rows):
+        if k == len(rows) - 1 and end & F.END_NO_MOVES:
+            mated = bool(end & (F.END_CHECK | F.END_EXTINCT))
+            assert (r.score.kind, r.score.value, r.depth, r.nodes) == ("mate" if mated else "cp", 0, 0, 0)
+            assert r.best_move is None
+        else:
+            assert (r.score.kind, r.score.value, r.depth, r.nodes) == ("cp", cp(ps[k], po[k]), 0, 1)
+    return end
 
 
 def test_analysis_batches_match_oracle(chan):
@@ -51,12 +82,47 @@ def test_analysis_batches_match_oracle(chan):
     assert len(res) == len(bodies)
     for b, rows in zip(bodies, res):
         assert not isinstance(rows, B.PositionFailed), rows
-        ps, po = expect(on, b.position, b.moves)
-        assert [r.position_id for r in rows] == list(range(len(ps)))
-        assert [r.psqt for r in rows] == ps.tolist()
-        assert [r.positional for r in rows] == po.tolist()
-        assert [r.score.value for r in rows] == [cp(a, c) for a, c in zip(ps, po)]
-        assert all(r.depth == 0 and r.nodes == 1 and r.score.kind == "cp" for r in rows)
+        check_rows(on, b, rows)
+
+
+def test_games_that_end_on_the_board(chan):
+    """Checkmate -> mate 0, stalemate -> cp 0 on the last ply (and a root that
+    is already mated), as Stockfish answers `go` there; JSON {"mate":0}."""
+    stub, on = chan
+    bodies = [B.AcquireResponseBody("mate", START, FOOLS_MATE),
+              B.AcquireResponseBody("stalemate", STALEMATE[0], STALEMATE[1], variant="fromPosition"),
+              B.AcquireResponseBody("mated-root", "rnb1kbnr/pppp1ppp/8/4p3/6Pq/5P2/PPPPP2P/RNBQKBNR w KQkq - 1 3", "")]
+    res = stub.go(bodies)
+    ends = [check_rows(on, b, rows) for b, rows in zip(bodies, res)]
+    assert ends == [F.END_NO_MOVES | F.END_CHECK, F.END_NO_MOVES, F.END_NO_MOVES | F.END_CHECK]
+    assert res[0][-1].score == B.Score("mate", 0) and res[1][-1].score == B.Score("cp", 0)
+    parts = json.loads(B.into_analysis(res[0]))
+    assert parts[-1]["score"] == {"mate": 0} and parts[-1]["depth"] == 0 and parts[-2]["score"].keys() == {"cp"}
+
+
+def test_variant_analysis_batches(chan):
+    """Crazyhouse and atomic batches on their own nets, every ply against the
+    variant oracle; atomic games that end by an explosion answer mate 0 there
+    (the kingless last ply no longer fails the batch)."""
+    stub, on = chan
+    bodies, kinds = [], []
+    for i in range(24):
+        for variant, name, fen in ((ZH, "crazyhouse", ZH_START), (AT, "atomic", START)):
+            moves = F.random_vgame(1000 + i, variant, fen, 30 + 9 * i)
+            bodies.append(B.AcquireResponseBody(f"{name}{i}", fen, moves, variant=name))
+            kinds.append(variant)
+    bodies.append(B.AcquireResponseBody("boom", START, ATOMIC_WIN, variant="atomic"))
+    kinds.append(AT)
+    bodies.append(B.AcquireResponseBody("chess", START, "e2e4 e7e5"))
+    kinds.append(0)
+    res = stub.go(bodies)
+    extinct = 0
+    for b, rows, variant in zip(bodies, res, kinds):
+        assert not isinstance(rows, B.PositionFailed), (b.batch_id, rows)
+        end = check_rows(on, b, rows, variant)
+        extinct += bool(end & F.END_EXTINCT)
+    assert extinct >= 2  # the explicit one and random games that ended by an explosion
+    assert res[-2][-1].score == B.Score("mate", 0) and (res[-2][-1].psqt, res[-2][-1].positional) == (0, 0)
 
 
 def test_failed_batches_are_isolated(chan):
@@ -67,15 +133,17 @@ def test_failed_batches_are_isolated(chan):
         B.AcquireResponseBody("badmove", START, "e2e4 e7e5 e1e3"),
         good,
         B.AcquireResponseBody("badfen", "rnbqkbnr/pppppppp/8/8 w", "e2e4"),
-        B.AcquireResponseBody("zh", START, "e2e4", variant="crazyhouse"),
+        B.AcquireResponseBody("anti", START, "e2e4", variant="antichess"),
         B.AcquireResponseBody("mpv", START, "e2e4", multipv=3),
         B.AcquireResponseBody("threekings", "4k3/8/8/8/8/8/8/K3K3 w - - 0 1", ""),
         B.AcquireResponseBody("good2", START, "d2d4 d7d5 c2c4"),
+        B.AcquireResponseBody("zhbad", ZH_START, "e2e4 P@e4", variant="crazyhouse"),
+        B.AcquireResponseBody("zhgood", ZH_START, "e2e4 d7d5 e4d5 d8d5 P@e4", variant="crazyhouse"),
     ]
     res = stub.go(bodies)
     codes = {b.batch_id: (r.code if isinstance(r, B.PositionFailed) else 0) for b, r in zip(bodies, res)}
-    assert codes["badmove"] == -8 and codes["badfen"] == -9
-    assert codes["zh"] == -1 and codes["mpv"] == 0  # MultiPV: answered in the matrix form (one line)
+    assert codes["badmove"] == -8 and codes["badfen"] == -9 and codes["zhbad"] == -8
+    assert codes["anti"] == -4 and codes["mpv"] == 0  # MultiPV: answered in the matrix form (one line)
     mpv = res[4]
     assert len(mpv) == 2 and all(r.matrix for r in mpv)
     ps, po = expect(on, START, "e2e4")
@@ -83,12 +151,29 @@ def test_failed_batches_are_isolated(chan):
     m = json.loads(B.into_analysis(mpv))
     assert m[0]["pv"] == [[[]]] and m[0]["score"] == [[{"cp": mpv[0].score.value}]] and m[0]["depth"] == 0
     assert codes["threekings"] != 0
-    assert codes["good"] == 0 and codes["good2"] == 0
+    assert codes["good"] == 0 and codes["good2"] == 0 and codes["zhgood"] == 0
     for i in (1, 6):
-        ps, po = expect(on, bodies[i].position, bodies[i].moves)
-        assert [r.psqt for r in res[i]] == ps.tolist() and [r.positional for r in res[i]] == po.tolist()
+        check_rows(on, bodies[i], res[i])
+    check_rows(on, bodies[8], res[8], ZH)
     with pytest.raises(B.PositionFailed):
         stub.go_one(bodies[0])
+
+
+def test_variant_batch_without_its_net():
+    """A chess-only backend fails crazyhouse / atomic batches (FNNUE_E_ARCH)
+    and evaluates the chess ones; a net in the wrong slot is refused."""
+    data = net_bytes(1, 256, 0)
+    stub, actor = B.channel(F.Net.from_bytes(data), 0)
+    try:
+        res = stub.go([B.AcquireResponseBody("zh", ZH_START, "e2e4", variant="crazyhouse"),
+                       B.AcquireResponseBody("at", START, "e2e4", variant="atomic"),
+                       B.AcquireResponseBody("std", START, "e2e4")])
+        assert res[0].code == -4 and res[1].code == -4 and not isinstance(res[2], B.PositionFailed)
+    finally:
+        actor.close()
+    with pytest.raises(F.FnnueError) as e:
+        B.channel(None, 0, crazyhouse=F.Net.from_bytes(data))
+    assert e.value.name == "FNNUE_E_ARCH"
 
 
 def test_skip_positions_and_all_skipped(chan):
@@ -109,21 +194,56 @@ def test_skip_positions_and_all_skipped(chan):
     assert all(r.skipped for r in allskip)
 
 
+def search1(on, fen, moves, variant=0):
+    """The one-ply search the backend runs, restated: mates first, stalemates
+    0, else -v(child); first maximum."""
+    if variant == 0:
+        pos, off = F.game_children(fen, moves)
+    else:
+        pos, off = F.game_vchildren(variant, fen, moves)
+    kids = pos[off[-2] + 1: off[-1]]
+    ps, po, rc = on[variant].eval_packed(kids, threads=8)
+    return kids, ps, po
+
+
 def test_move_work_best_child(chan):
     stub, on = chan
     for k, g in enumerate(GAMES[:6]):
         mv = " ".join(g["moves"].split()[: 10 + 7 * k])
         body = B.AcquireResponseBody(f"m{k}", g["position"], mv, work="move")
         (r,) = stub.go_one(body)
-        pos, off = F.game_children(g["position"], mv)
-        kids = pos[off[-2] + 1: off[-1]]
-        ps, po, rc = on.eval_packed(kids, threads=8)
+        kids, ps, po = search1(on, g["position"], mv)
         vals = [-int((int(a) + int(b)) / 16) for a, b in zip(ps, po)]
-        best = int(np.argmax(vals))  # first maximum, as the backend
+        best = int(np.argmax(vals))  # first maximum, as the backend (no mate in one in these positions)
         assert r.nodes == len(kids) and r.depth == 1
-        assert r.score.value == int(vals[best] * 100 / 361)
+        assert r.score == B.Score("cp", int(vals[best] * 100 / 361))
         after = F.game_positions(g["position"], (mv + " " + r.best_move).strip())[-1]
         assert np.array_equal(after, kids[best]), (r.best_move, best)
+
+
+def test_move_work_mates_and_terminal_roots(chan):
+    """Move work: a mate in one is played (score mate 1) whatever the NNUE
+    says about the other children; atomic: the exploding capture; a root
+    with no legal move has no best move (mate 0 / cp 0)."""
+    stub, on = chan
+    bodies = [B.AcquireResponseBody("m1", START, "f2f3 e7e5 g2g4", work="move"),
+              B.AcquireResponseBody("at1", START, "g1f3 e7e6 f3g5 f8e7", work="move", variant="atomic"),
+              B.AcquireResponseBody("mated", START, FOOLS_MATE, work="move"),
+              B.AcquireResponseBody("stale", STALEMATE[0], STALEMATE[1], work="move"),
+              B.AcquireResponseBody("boom", START, ATOMIC_WIN, work="move", variant="atomic"),
+              B.AcquireResponseBody("zh", ZH_START, "e2e4 d7d5 e4d5 d8d5", work="move", variant="crazyhouse")]
+    res = [r[0] for r in stub.go(bodies)]
+    assert res[0].best_move == "d8h4" and res[0].score == B.Score("mate", 1) and res[0].depth == 1
+    assert res[1].score == B.Score("mate", 1)
+    assert F.game_end(START, bodies[1].moves + " " + res[1].best_move, AT) & F.END_EXTINCT
+    for r, kind in ((res[2], "mate"), (res[3], "cp"), (res[4], "mate")):
+        assert r.best_move is None and r.score == B.Score(kind, 0) and (r.depth, r.nodes) == (0, 0)
+    kids, ps, po = search1(on, ZH_START, bodies[5].moves, ZH)
+    vals = [-int((int(a) + int(b)) / 16) for a, b in zip(ps, po)]
+    assert res[5].nodes == len(kids) > 0
+    assert res[5].score == B.Score("cp", int(max(vals) * 100 / 361))
+    after = F.game_vpositions(ZH, ZH_START, bodies[5].moves + " " + res[5].best_move)[-1]
+    assert np.array_equal(after, kids[int(np.argmax(vals))])
 
 
 def test_concurrent_callers(chan):
@@ -141,5 +261,4 @@ def test_concurrent_callers(chan):
         t.join()
     for t in range(4):
         for b, rows in zip(bodies[t * 5:(t + 1) * 5], out[t]):
-            ps, po = expect(on, b.position, b.moves)
-            assert [r.psqt for r in rows] == ps.tolist() and [r.positional for r in rows] == po.tolist()
+            check_rows(on, b, rows)

@@ -86,6 +86,30 @@ def test_variant_invalid_position_and_wrong_entry_point(vcache):
     assert e.value.name == "FNNUE_E_ARCH"
 
 
+def test_atomic_game_over_records(vcache):
+    """An atomic position with one king exploded is the game's end, not an
+    error: (0, 0) on both entry points and in groups, the rest evaluated as
+    usual; a position with no king at all still fails, naming its index
+    (ADVICE r03)."""
+    ev, on = vcache(ATOMIC)
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    moves = "g1f3 e7e6 f3g5 f8e7 g5f7"  # Nxf7 explodes the black king on e8
+    assert F.game_end(start, moves, variant=ATOMIC) == F.END_NO_MOVES | F.END_EXTINCT
+    pos = F.game_vpositions(ATOMIC, start, moves)
+    ps, po = ev.eval_vpositions(pos)
+    assert ps[-1] == 0 and po[-1] == 0 and np.any(po[:-1])
+    ops, opo, rc = on.eval_packed(pos)
+    assert rc == 0 and np.array_equal(ps, ops) and np.array_equal(po, opo)
+    gs, go = ev.eval_vgroups(pos, np.array([0, len(pos)], np.uint32))
+    assert np.array_equal(gs, ps) and np.array_equal(go, po)
+    bad = np.concatenate([pos, pos[-1:]])
+    bad[-1, :32] &= np.where((bad[-1, :32] & 15) == 6, 0xF0, 0xFF).astype(np.uint8)  # drop the white king too
+    bad[-1, :32] &= np.where((bad[-1, :32] >> 4) == 6, 0x0F, 0xFF).astype(np.uint8)
+    with pytest.raises(F.FnnueError) as e:
+        ev.eval_vpositions(bad)
+    assert e.value.name == "FNNUE_E_POSITION" and f"index {len(pos)}" in str(e.value)
+
+
 def test_variant_full_batch(vcache):
     """1M crazyhouse positions in one call (the config-2 batch size), sampled
     against the oracle, and the device entry point agrees with the host one."""

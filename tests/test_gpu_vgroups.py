@@ -44,11 +44,22 @@ def legal_games(variant, count, seed, plies=160):
     return games, np.concatenate(parts), off
 
 
-def valid_mask(pos):
+def kings(pos):
     b = np.zeros((len(pos), 64), np.uint8)
     b[:, 0::2] = pos[:, :32] & 15
     b[:, 1::2] = pos[:, :32] >> 4
-    return ((b == 6).sum(1) == 1) & ((b == 14).sum(1) == 1)
+    return (b == 6).sum(1) + (b == 14).sum(1)
+
+
+def check_game_over(variant, pos, ps, po):
+    """Atomic game-over records (one king exploded) are kept and answered with
+    (0, 0); crazyhouse never loses a king."""
+    k = kings(pos)
+    if variant == AT:
+        assert np.any(k == 1)
+        assert not np.any(ps[k == 1]) and not np.any(po[k == 1])
+    else:
+        assert np.all(k == 2)
 
 
 @pytest.mark.parametrize("variant", [ZH, AT])
@@ -58,12 +69,9 @@ def test_vgroups_chain_legal_games_match_oracle(vc, variant, hd):
     equals the from-scratch GPU path and the oracle."""
     ev, on = vc(variant, hd)
     _, pos, off = legal_games(variant, 400, 7 * hd + variant)
-    ok = valid_mask(pos)
-    if not ok.all():  # atomic: a game that ends with an exploded king; keep only complete games
-        keep = [g for g in range(len(off) - 1) if ok[off[g]:off[g + 1]].all()]
-        pos = np.concatenate([pos[off[g]:off[g + 1]] for g in keep])
-        off = np.concatenate([[0], np.cumsum([off[g + 1] - off[g] for g in keep])]).astype(np.uint32)
+    # atomic games that end by an explosion keep their last ply (ADVICE r03)
     gs, go = ev.eval_vgroups(pos, off, N.GROUP_CHAIN)
+    check_game_over(variant, pos, gs, go)
     ss, so = ev.eval_vpositions(pos)
     assert np.array_equal(gs, ss) and np.array_equal(go, so)
     ops, opo, rc = on.eval_packed(pos, threads=8)
@@ -82,16 +90,13 @@ def test_vgroups_star_children_match_oracle(vc, variant):
         parts.append(p)
         offs.append(o[1:].astype(np.int64) + base)
         base += len(p)
-    pos, off = np.concatenate(parts), np.concatenate(offs).astype(np.int64)
-    ok = valid_mask(pos)
-    if not ok.all():  # atomic: children that explode a king have no accumulator; drop them from their groups
-        keep = np.nonzero(ok)[0]
-        gid = np.repeat(np.arange(len(off) - 1), np.diff(off))[keep]
-        pos = pos[keep]
-        off = np.concatenate([[0], np.cumsum(np.bincount(gid, minlength=len(off) - 1))])
-    off = off.astype(np.uint32)
-    assert valid_mask(pos).all()
+    pos, off = np.concatenate(parts), np.concatenate(offs).astype(np.uint32)
+    # atomic: every child that captures next to the enemy king is a game-over
+    # record inside its STAR group (kept, answered (0, 0))
     gs, go = ev.eval_vgroups(pos, off, N.GROUP_STAR)
+    check_game_over(variant, pos, gs, go)
+    ss, so = ev.eval_vpositions(pos)
+    assert np.array_equal(gs, ss) and np.array_equal(go, so)
     ops, opo, rc = on.eval_packed(pos, threads=8)
     assert rc == 0 and np.array_equal(gs, ops) and np.array_equal(go, opo)
 

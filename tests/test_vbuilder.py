@@ -203,7 +203,8 @@ def test_variant_builder_entry_points_without_gpu():
 def test_random_vgames_deterministic_and_replayable(variant):
     """fnnue_random_vgames (bench / test inputs): every ply of legal random games
     as CHAIN groups, independent of the thread count; each game's first
-    position is the start position, every position has both kings."""
+    position is the start position, every position has both kings except an
+    atomic game's last one when a king exploded there (the game's end)."""
     a, oa = nnue.random_vgames(9, variant, 300, 120, threads=1)
     b, ob = nnue.random_vgames(9, variant, 300, 120, threads=7)
     assert np.array_equal(a, b) and np.array_equal(oa, ob)
@@ -213,6 +214,14 @@ def test_random_vgames_deterministic_and_replayable(variant):
     bd = np.zeros((len(a), 64), np.uint8)
     bd[:, 0::2] = a[:, :32] & 15
     bd[:, 1::2] = a[:, :32] >> 4
-    assert np.all((bd == 6).sum(1) == 1) and np.all((bd == 14).sum(1) == 1)
+    kings = (bd == 6).sum(1) + (bd == 14).sum(1)
+    last = np.zeros(len(a), bool)
+    last[oa[1:].astype(np.int64) - 1] = True
+    assert np.all(((bd == 6).sum(1) <= 1) & ((bd == 14).sum(1) <= 1))
+    assert np.all(kings[~last] == 2)
+    if variant == AT:
+        assert np.any(kings[last] == 1)  # some games end by explosion
+    else:
+        assert np.all(kings == 2)
     if variant == ZH:
         assert int(a[:, 33:43].sum()) > 0  # pockets fill up
