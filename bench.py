@@ -79,6 +79,9 @@ def parse_args():
     ap.add_argument("--small-net", type=int, default=0, metavar="HD",
                     help="also evaluate every position with a second (small) net of this width each step "
                          "(BASELINE config 3: big + small net; later Stockfish's small net is HD 128)")
+    ap.add_argument("--no-dual", action="store_true",
+                    help="with --small-net on groups: two evaluation calls per step instead of one "
+                         "fnnue_eval_groups_dual_device call (A/B)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -398,7 +401,18 @@ def main():
     # input copies); one process launch: no host sync between devices
     streams = [torch.cuda.current_stream(torch.device("cuda", d)).cuda_stream for d in devices]
 
+    # Big + small net over groups on one GPU: one call, one plan
+    # (fnnue_eval_groups_dual_device; the small net's FT and stacks overlap
+    # the big net's stacks on the small context's stream).
+    dual = bool(args.small_net) and groups and launch == "single" and variant is None and not args.no_dual
+
     def step():
+        if dual:
+            s, e = shards[0], evs[0][0]
+            e.eval_groups_dual_device(evs[1][0], s.pos.data_ptr(), s.off.data_ptr(), s.ng, s.n, gmode,
+                                      s.psqt.data_ptr(), s.positional.data_ptr(), s.small[0].data_ptr(),
+                                      s.small[1].data_ptr(), torch.cuda.current_stream().cuda_stream)
+            return
         for k in range(len(evs)):
             run_net(k)
 
@@ -623,9 +637,11 @@ def main():
     main_k = MAIN_KERNEL[("groups" if groups else "positions", impl)]
     counters, src, tree_ok = None, None, None
     cpath = os.path.join(ROOT, "profiles", "counters.json")
-    if os.path.exists(cpath) and args.hd == 1024 and not args.small_net:
-        db = json.load(open(cpath))
-        counters = db.get("workloads", {}).get(args.workload)
+    db = json.load(open(cpath)) if os.path.exists(cpath) else {}
+    # counters are keyed by workload, "<workload>@<hd>" for widths other than 1024
+    ckey = args.workload if args.hd == 1024 else f"{args.workload}@{args.hd}"
+    if db:
+        counters = db.get("workloads", {}).get(ckey)
         src = db.get("source")
         tree_ok = db.get("tree") == tree_hash()
     kernels = {}
@@ -654,6 +670,21 @@ def main():
                 "2.4 GHz spec clock); gather_equivalent_GBps = SURVEY §8d algorithmic bytes (every feature row "
                 "read from memory) over the same time: the sliced kernels read rows from LDS tiles, so it may "
                 "exceed the 8 TB/s HBM peak"})
+
+    if small is not None:
+        # the small net's own feature-transformer roofline: its counters (profiled
+        # alone at its width) over its live kernel time in this run
+        sc = db.get("workloads", {}).get(f"{args.workload}@{args.small_net}", {}).get(main_k, {}).get("counters")
+        sft = small["ft_kernel_avg_ms"]
+        if sc and sft > 0:
+            sfr = resource_fractions(sc, sft * 1e-3)
+            sb = max(sfr, key=lambda k: sfr[k]["frac"])
+            small["roofline"] = {"kernel": main_k, "bound": sb, "frac": sfr[sb]["frac"], "fractions": sfr,
+                                 "counters": {"source": db.get("source"), "tree_matches": tree_ok,
+                                              "key": f"{args.workload}@{args.small_net}"}}
+        small["how"] = ("one fnnue_eval_groups_dual_device call per step: one plan, the small net's FT + stacks on "
+                        "the small context's stream beside the big net's stacks" if dual else
+                        "a second evaluation call per step on the small net's context")
 
     if rank == 0:
         out = {

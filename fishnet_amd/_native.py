@@ -78,6 +78,7 @@ SIGNATURES = {
     "fnnue_eval_groups": ([_vp, _vp, _sz, _vp, _sz, _i32, _vp, _vp], _i32),
     "fnnue_eval_positions_device": ([_vp, _vp, _sz, _vp, _vp, _vp], _i32),
     "fnnue_eval_groups_device": ([_vp, _vp, _vp, _sz, _sz, _i32, _vp, _vp, _vp], _i32),
+    "fnnue_eval_groups_dual_device": ([_vp, _vp, _vp, _vp, _sz, _sz, _i32, _vp, _vp, _vp, _vp, _vp], _i32),
     "fnnue_ctx_check": ([_vp], _i32),
     "fnnue_pos_from_fen": ([C.c_char_p, _vp], _i32),
     "fnnue_game_positions": ([C.c_char_p, C.c_char_p, _vp, _sz, _P(_sz)], _i32),

@@ -62,7 +62,8 @@ void ctx_destroy(fnnue_ctx* c) {
   for (auto& quad : c->evpool)
     for (auto e : quad)
       if (e) (void)hipEventDestroy(e);
-  if (c->ws_event) (void)hipEventDestroy(c->ws_event);
+  for (hipEvent_t e : {c->ws_event, c->dual_fork, c->dual_join})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off, (void*)c->d_btext,
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
@@ -342,6 +343,14 @@ struct WorkspaceUse {
       c->ws_own_pending = true;
     } else if (hipEventRecord(c->ws_event, s) == hipSuccess) {
       c->ws_recorded = true;
+      c->ws_own_pending = false;
+    } else {
+      // No event for this call's work: the stale one (an earlier call's) would
+      // let the next call on another stream overwrite the workspace while this
+      // one still reads it.  Wait for the work instead (a destructor cannot
+      // return the error; the ordering is what must hold).
+      (void)hipStreamSynchronize(s);
+      c->ws_recorded = false;
       c->ws_own_pending = false;
     }
   }
@@ -745,9 +754,91 @@ int eval_groups_device(fnnue_ctx* ctx, const void* d_pos, size_t pos_bytes, cons
   return FNNUE_OK;
 }
 
+// Big + small net over the same CHAIN / STAR batch ("dual NNUE": both nets
+// read the same HalfKAv2_hm features and update their accumulators from the
+// same deltas, upstream evaluate_nnue.cpp with two networks).  The plan
+// (group spans, deltas, segments, lists, units) is built once in the big
+// context's workspace on the call's stream s; then s forks: the small net's
+// main kernel and stacks run on the small context's stream over that plan
+// while s runs the big net's main kernel and stacks (the small net's few
+// hundred (unit, slice) workgroups interleave with the big net's thousands on
+// the CUs), and s joins before the next chunk's plan overwrites what the small
+// FT reads.  (Forking after the big net's main kernel instead, so that the
+// small FT ran beside the big net's stacks only, measured 878M against 928M
+// plies/s for two independent calls: the small FT then sat on the critical
+// path.)
+int eval_groups_dual_device(fnnue_ctx* a, fnnue_ctx* b, const fnnue_pos* d_pos, const uint32_t* d_off, size_t ngroups,
+                            size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, int32_t* d_psqt2,
+                            int32_t* d_positional2, void* stream) {
+  if (!a || !b) return fail(FNNUE_E_ARG, "null ctx");
+  if (a == b) return fail(FNNUE_E_ARG, "the two nets need two contexts");
+  if (a->variant != kVariantChess || b->variant != kVariantChess)
+    return fail(FNNUE_E_ARCH, "dual evaluation: two chess (HalfKAv2_hm) nets");
+  if (a->device != b->device) return fail(FNNUE_E_ARG, "the two contexts must be on one device");
+  if (a->ft_impl != FNNUE_FT_SLICED || b->ft_impl != FNNUE_FT_SLICED)
+    return fail(FNNUE_E_ARG, "dual evaluation runs on the sliced feature transformer");
+  if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
+  if (ngroups == 0) return npos == 0 ? FNNUE_OK : fail(FNNUE_E_ARG, "positions without groups");
+  if (ngroups > 0xFFFFFFFFu || npos > 0xFFFFFFFFu) return fail(FNNUE_E_ARG, "batch too large");
+  if (!d_pos || !d_off || !d_psqt || !d_positional || !d_psqt2 || !d_positional2)
+    return fail(FNNUE_E_ARG, "null buffer");
+  DeviceGuard g(a->device);
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : a->stream;
+  hipStream_t s2 = b->stream;
+  int rc = order_workspace(a, s);
+  if (rc || (rc = order_workspace(b, s2))) return rc;
+  WorkspaceUse use_a{a, s};
+  WorkspaceUse use_b{b, s2};
+  if ((rc = ensure_seg(a)) || (rc = ensure_span(a, npos))) return rc;
+  for (fnnue_ctx* c : {a})
+    for (hipEvent_t* e : {&c->dual_fork, &c->dual_join})
+      if (!*e) HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate");
+  HIP_TRY(launch_group_span(d_off, (uint32_t)ngroups, (uint32_t)npos, a->seg.span, true, a->err, s),
+          "group_span launch");
+  const uint2* span = static_cast<const uint2*>(a->seg.span);
+  const uint32_t chunk = std::min(a->chunk, b->chunk);
+  // the small net over the big context's plan: its own tiles, SWAR flag and PSQT parts
+  SlicedPlan pb = a->plan;
+  pb.tiles = b->plan.tiles;
+  pb.swar = b->plan.swar;
+  pb.psqt_part = b->plan.psqt_part;
+  for (size_t i0 = 0; i0 < npos; i0 += chunk) {
+    const uint32_t m = (uint32_t)std::min<size_t>(chunk, npos - i0);
+    std::array<hipEvent_t, 4>*ev = nullptr, *ev2 = nullptr;
+    if ((rc = next_events(a, &ev)) || (rc = next_events(b, &ev2))) return rc;
+    if ((rc = record_event(a, ev, 0, s))) return rc;
+    HIP_TRY(launch_seg_plan(kVariantChess, d_pos + i0, m, span + i0, (uint32_t)i0, mode, a->plan, a->seg, a->bucket,
+                            a->err, s),
+            "segment plan launch");
+    HIP_TRY(hipEventRecord(a->dual_fork, s), "hipEventRecord");
+    HIP_TRY(hipStreamWaitEvent(s2, a->dual_fork, 0), "hipStreamWaitEvent");
+    if ((rc = record_event(a, ev, 1, s))) return rc;
+    HIP_TRY(launch_seg_ft(a->hd, kVariantChess, m, mode, a->ptrs, a->plan, a->seg, a->x, s), "ft_segments launch");
+    // the small net has no plan of its own: its plan phase is empty
+    if ((rc = record_event(b, ev2, 0, s2)) || (rc = record_event(b, ev2, 1, s2))) return rc;
+    HIP_TRY(launch_seg_ft(b->hd, kVariantChess, m, mode, b->ptrs, pb, a->seg, b->x, s2), "ft_segments launch");
+    if ((rc = record_event(b, ev2, 2, s2))) return rc;
+    HIP_TRY(launch_stack(b->hd, b->x, a->bucket, m, b->ptrs, d_positional2 + i0, nullptr, b->plan.psqt_part,
+                         d_psqt2 + i0, s2),
+            "stack kernel launch");
+    if ((rc = record_event(b, ev2, 3, s2))) return rc;
+    HIP_TRY(hipEventRecord(a->dual_join, s2), "hipEventRecord");
+    if ((rc = run_chunk_tail(a, m, d_positional + i0, s, ev, nullptr, a->plan.psqt_part, d_psqt + i0))) return rc;
+    HIP_TRY(hipStreamWaitEvent(s, a->dual_join, 0), "hipStreamWaitEvent");
+  }
+  return FNNUE_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int fnnue_eval_groups_dual_device(fnnue_ctx* big, fnnue_ctx* small, const fnnue_pos* d_pos, const uint32_t* d_off,
+                                  size_t ngroups, size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional,
+                                  int32_t* d_psqt_small, int32_t* d_positional_small, void* stream) {
+  return eval_groups_dual_device(big, small, d_pos, d_off, ngroups, npos, mode, d_psqt, d_positional, d_psqt_small,
+                                 d_positional_small, stream);
+}
 
 int fnnue_eval_groups_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, const uint32_t* d_off, size_t ngroups,
                              size_t npos, int mode, int32_t* d_psqt, int32_t* d_positional, void* stream) {

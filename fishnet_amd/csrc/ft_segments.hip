@@ -875,9 +875,13 @@ hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, 
 
 }  // namespace
 
-// units close at kSegUnitPlies positions (>= 1 item each) or kUnitItems items;
-// a unit holding fewer than kSegUnitPlies / 160 items is its king block's last
-uint32_t seg_max_units(uint32_t chunk) { return 64 + (2 * chunk + kSegUnitPlies / 160 - 1) / (kSegUnitPlies / 160); }
+// units close at kSegUnitPlies of work, an item weighing at most
+// seg_bin_weight(32): a unit holding fewer than kSegUnitPlies / that many items
+// is its king block's last
+uint32_t seg_max_units(uint32_t chunk) {
+  constexpr uint32_t per = kSegUnitPlies / seg_bin_weight(32);
+  return 64 + (2 * chunk + per - 1) / per;
+}
 
 size_t seg_ctr_words() {
   return std::max({SegCtr<ChessFs>::kWords, SegCtr<VariantFs<kVariantCrazyhouse>>::kWords,
@@ -908,42 +912,54 @@ hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npo
   return hipGetLastError();
 }
 
-hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase,
-                              int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
-                              uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid) {
+hipError_t launch_seg_plan(int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase, int mode,
+                           const SlicedPlan& P, const SegPlan& G, uint8_t* bucket, uint32_t* err, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const bool star = mode == FNNUE_GROUP_STAR;
   const uint2* sp = static_cast<const uint2*>(span);
+  if (variant == kVariantChess)
+    return seg_plan_t<ChessFs>(static_cast<const fnnue_pos*>(pos), n, sp, sbase, star, P, G, bucket, err, stream);
+  const fnnue_vpos* vp = static_cast<const fnnue_vpos*>(pos);
+  if (variant == kVariantCrazyhouse)
+    return seg_plan_t<VariantFs<kVariantCrazyhouse>>(vp, n, sp, sbase, star, P, G, bucket, err, stream);
+  if (variant == kVariantAtomic)
+    return seg_plan_t<VariantFs<kVariantAtomic>>(vp, n, sp, sbase, star, P, G, bucket, err, stream);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_seg_ft(uint32_t hd, int variant, uint32_t n, int mode, const NetPtrs& net, const SlicedPlan& P,
+                         const SegPlan& G, uint8_t* x, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const bool star = mode == FNNUE_GROUP_STAR;
   const uint32_t mu = seg_max_units(n);
-  hipError_t e;
-  auto mark = [&]() { return mid ? hipEventRecord(mid, stream) : hipSuccess; };
   if (variant == kVariantChess) {
-    if ((e = seg_plan_t<ChessFs>(static_cast<const fnnue_pos*>(pos), n, sp, sbase, star, P, G, bucket, err, stream)) !=
-            hipSuccess ||
-        (e = mark()) != hipSuccess)
-      return e;
 #define CALL(H) ft_segments_t<H, ChessFs>(G, P, net, n, star, x, mu, stream)
     FNNUE_HD_DISPATCH(hd, CALL)
 #undef CALL
   }
-  const fnnue_vpos* vp = static_cast<const fnnue_vpos*>(pos);
-#define FNNUE_VSEG(V)                                                                                      \
-  {                                                                                                        \
-    using Fs = VariantFs<V>;                                                                               \
-    if ((e = seg_plan_t<Fs>(vp, n, sp, sbase, star, P, G, bucket, err, stream)) != hipSuccess ||           \
-        (e = mark()) != hipSuccess)                                                                        \
-      return e;                                                                                            \
-    switch (hd) {                                                                                          \
-      case 256: return ft_segments_t<256, Fs>(G, P, net, n, star, x, mu, stream);                          \
-      case 512: return ft_segments_t<512, Fs>(G, P, net, n, star, x, mu, stream);                          \
-      case 1024: return ft_segments_t<1024, Fs>(G, P, net, n, star, x, mu, stream);                        \
-      default: return hipErrorInvalidValue;                                                                \
-    }                                                                                                      \
+#define FNNUE_VSEG(V)                                                                    \
+  {                                                                                      \
+    using Fs = VariantFs<V>;                                                             \
+    switch (hd) {                                                                        \
+      case 256: return ft_segments_t<256, Fs>(G, P, net, n, star, x, mu, stream);        \
+      case 512: return ft_segments_t<512, Fs>(G, P, net, n, star, x, mu, stream);        \
+      case 1024: return ft_segments_t<1024, Fs>(G, P, net, n, star, x, mu, stream);      \
+      default: return hipErrorInvalidValue;                                              \
+    }                                                                                    \
   }
   if (variant == kVariantCrazyhouse) FNNUE_VSEG(kVariantCrazyhouse)
   if (variant == kVariantAtomic) FNNUE_VSEG(kVariantAtomic)
 #undef FNNUE_VSEG
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase,
+                              int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
+                              uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid) {
+  if (n == 0) return hipSuccess;
+  hipError_t e = launch_seg_plan(variant, pos, n, span, sbase, mode, P, G, bucket, err, stream);
+  if (e == hipSuccess && mid) e = hipEventRecord(mid, stream);
+  return e != hipSuccess ? e : launch_seg_ft(hd, variant, n, mode, net, P, G, x, stream);
 }
 
 }  // namespace fnnue

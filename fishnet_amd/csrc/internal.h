@@ -56,6 +56,10 @@ struct fnnue_ctx {
   // the context) and recorded no event: a call on the same stream needs no
   // ordering, one on another stream records ws_event on `stream` first.
   bool ws_own_pending = false;
+  // fnnue_eval_groups_dual_device: this context (the big net) plans, the
+  // small net's main kernel and stacks run on the small context's stream
+  // between dual_fork (after this net's main kernel) and dual_join.
+  hipEvent_t dual_fork = nullptr, dual_join = nullptr;
 };
 
 

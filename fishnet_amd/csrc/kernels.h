@@ -126,6 +126,14 @@ hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npo
 hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase,
                               int mode, const NetPtrs& net, const SlicedPlan& P, const SegPlan& G, uint8_t* x,
                               uint8_t* bucket, uint32_t* err, hipStream_t stream, hipEvent_t mid = nullptr);
+// Its two halves.  The plan depends on the positions, the groups and the
+// feature set only, not on the net: a second net of the same feature set (the
+// small net beside the big one) runs its main kernel over the same plan
+// (P.ctr / units / flist and G), with its own tiles, swar flag, psqt_part, x.
+hipError_t launch_seg_plan(int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase, int mode,
+                           const SlicedPlan& P, const SegPlan& G, uint8_t* bucket, uint32_t* err, hipStream_t stream);
+hipError_t launch_seg_ft(uint32_t hd, int variant, uint32_t n, int mode, const NetPtrs& net, const SlicedPlan& P,
+                         const SegPlan& G, uint8_t* x, hipStream_t stream);
 
 // MFMA operand-layout self test: returns number of mismatching outputs in *bad.
 hipError_t run_mfma_selftest(int* bad);

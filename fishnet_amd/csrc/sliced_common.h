@@ -156,15 +156,29 @@ __host__ __device__ constexpr uint32_t seg_len_bin(uint32_t L) {
   return L <= 16 ? L - 1 : L <= 144 ? 16 + (L - 17) / 8 : 32;
 }
 // Segment units: contiguous item ranges of one king block holding about
-// kSegUnitPlies positions (items are sorted by length bin, a bin's items
-// counted at the bin's longest length), at most kUnitItems items.
+// kSegUnitPlies of work (items are sorted by length bin).  An item costs its
+// root refresh plus one delta step per further position: the refresh sums the
+// root's whole list (~25 rows, ~100 VALU per lane against ~27 for a delta
+// position), so an item may weigh kSegRootCost + the bin's longest length.
+// Counting positions alone (kSegRootCost 0) makes units of short segments
+// (king moves, STAR children that move the king: one refresh each) up to 3-6x
+// the work of the others (task timeline, tools/diag/seg_timeline.py,
+// profiles/r04g); weighing the refresh (4) evens the tasks out (longest 152 ->
+// 71 us on config 3) but not the kernel time: those long tasks start early and
+// the span is the total work plus one average task (A/B in profiles/r04h:
+// neutral on games, -2 % on children), so the default stays 0.
 #ifndef SEG_UNIT_PLIES
 #define SEG_UNIT_PLIES 16384
 #endif
+#ifndef SEG_ROOT_COST
+#define SEG_ROOT_COST 0
+#endif
 constexpr uint32_t kSegUnitPlies = SEG_UNIT_PLIES;
+constexpr uint32_t kSegRootCost = SEG_ROOT_COST;
 __host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
   return bin < 16 ? bin + 1 : bin < 32 ? 8 * bin - 104 : 160;
 }
+__host__ __device__ constexpr uint32_t seg_bin_weight(uint32_t bin) { return seg_bin_longest(bin) + kSegRootCost; }
 
 // Segment item bins per king block: 33 length bins x C classes of the root's
 // list length, so that the items of a pass, which all sum the pass's longest
@@ -233,14 +247,14 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
   auto kb_end = [&](int kb) -> uint32_t { return kb == KB - 1 ? s[KB * NB - 1] + ctr[KB * NB - 1] : s[(kb + 1) * NB]; };
   if (unit_items == 0) {
     // Segment units: unit u of king block kb starts at the first item whose
-    // cumulative positions (a bin's items counted at the bin's longest run)
-    // reach u * kSegUnitPlies.  Bins are contiguous in item order, so each
+    // cumulative work (a bin's items weighed seg_bin_weight) reaches
+    // u * kSegUnitPlies.  Bins are contiguous in item order, so each
     // (kb, bin) thread places the unit starts falling inside its bin.
     __shared__ uint32_t pb[kIB];        // positions before bin i within its king block
     __shared__ uint32_t ubase[KB + 1];  // first unit of each king block
     for (int k = 0; k < per; ++k) {     // local[k] = count of bin t*per + k
       const int i = t * per + k;
-      if (i < kIB) pb[i] = local[k] * seg_bin_longest(len_bin(i));
+      if (i < kIB) pb[i] = local[k] * seg_bin_weight(len_bin(i));
     }
     __syncthreads();
     if (t < KB) {
@@ -268,7 +282,7 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
       const int i = t * per + k;
       if (i >= kIB || local[k] == 0) continue;
       const int kb = i / NB;
-      const uint32_t w = seg_bin_longest(len_bin(i)), p0 = pb[i], p1 = p0 + local[k] * w;
+      const uint32_t w = seg_bin_weight(len_bin(i)), p0 = pb[i], p1 = p0 + local[k] * w;
       for (uint32_t u = (p0 + kSegUnitPlies - 1) / kSegUnitPlies; u * kSegUnitPlies < p1; ++u)
         units[ubase[kb] + u] = make_int4(kb, (int)(s[i] + (u * kSegUnitPlies - p0 + w - 1) / w), 0, 0);
     }

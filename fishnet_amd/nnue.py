@@ -297,6 +297,33 @@ class Evaluator:
         N.check(N.lib.fnnue_eval_groups_device(self._h, C.c_void_p(d_pos), C.c_void_p(d_off), ngroups, npos, mode,
                                                C.c_void_p(d_psqt), C.c_void_p(d_positional), C.c_void_p(stream)))
 
+    def eval_groups_dual_device(self, small: "Evaluator", d_pos: int, d_off: int, ngroups: int, npos: int, mode: int,
+                                d_psqt: int, d_positional: int, d_psqt_small: int, d_positional_small: int,
+                                stream: int | None):
+        """This (big) net and `small` over the same groups, one plan (fnnue_eval_groups_dual_device)."""
+        N.check(N.lib.fnnue_eval_groups_dual_device(self._h, small._h, C.c_void_p(d_pos), C.c_void_p(d_off), ngroups,
+                                                    npos, mode, C.c_void_p(d_psqt), C.c_void_p(d_positional),
+                                                    C.c_void_p(d_psqt_small), C.c_void_p(d_positional_small),
+                                                    C.c_void_p(stream)))
+
+    def eval_groups_dual(self, small: "Evaluator", pos: np.ndarray, off: np.ndarray, mode: int = N.GROUP_CHAIN):
+        """Host-buffer convenience over eval_groups_dual_device (torch for the device buffers)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        pos = np.ascontiguousarray(pos, dtype=np.uint8).reshape(-1, N.POS_BYTES)
+        off = np.ascontiguousarray(off, dtype=np.uint32)
+        n = len(pos)
+        d_pos = torch.from_numpy(pos).to(dev)
+        d_off = torch.from_numpy(off.view(np.int32)).to(dev)
+        out = torch.zeros((4, max(n, 1)), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        self.eval_groups_dual_device(small, d_pos.data_ptr(), d_off.data_ptr(), len(off) - 1, n, mode,
+                                     out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), None)
+        self.check()
+        small.check()
+        o = out[:, :n].cpu().numpy()
+        return o[0], o[1], o[2], o[3]
+
     def check(self) -> None:
         N.check(N.lib.fnnue_ctx_check(self._h))
 

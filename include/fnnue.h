@@ -289,6 +289,17 @@ int fnnue_eval_positions_device(fnnue_ctx *ctx, const fnnue_pos *d_pos, size_t n
                                 int32_t *d_positional, void *stream);
 int fnnue_eval_groups_device(fnnue_ctx *ctx, const fnnue_pos *d_pos, const uint32_t *d_off, size_t ngroups,
                              size_t npos, int mode, int32_t *d_psqt, int32_t *d_positional, void *stream);
+/* Big + small net over the same CHAIN / STAR batch (BASELINE config 3 "big +
+ * small net"; later Stockfish's dual NNUE evaluates a small HalfKAv2_hm net
+ * beside the big one on the same features): results identical to two
+ * fnnue_eval_groups_device calls, but the plan (deltas, segments, feature
+ * lists) is built once, in the big context's workspace, and the small net's
+ * feature transformer and layer stacks run on the small context's stream
+ * beside the big net's on `stream`.  Both contexts: chess nets on one device,
+ * sliced feature transformer.  No host synchronisation. */
+int fnnue_eval_groups_dual_device(fnnue_ctx *big, fnnue_ctx *small, const fnnue_pos *d_pos, const uint32_t *d_off,
+                                  size_t ngroups, size_t npos, int mode, int32_t *d_psqt, int32_t *d_positional,
+                                  int32_t *d_psqt_small, int32_t *d_positional_small, void *stream);
 /* Synchronises the ctx's device and reports (and clears) latched errors. */
 int fnnue_ctx_check(fnnue_ctx *ctx);
 

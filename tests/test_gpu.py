@@ -186,6 +186,55 @@ def test_random_games_chain_and_small_net(ev_cache):
         assert np.array_equal(ps, ops) and np.array_equal(po, opo)
 
 
+@pytest.mark.parametrize("big,small", [(1024, 128), (2048, 256), (1536, 128)])
+def test_dual_groups_big_and_small_net(ev_cache, big, small):
+    """fnnue_eval_groups_dual_device (BASELINE config 3's big + small net over
+    one plan, the small net on the small context's stream): identical to two
+    separate grouped calls and to the oracle, CHAIN and STAR, and across a
+    chunk boundary (> 2^20 positions)."""
+    eb, ob = ev_cache(1, big, 0)
+    es, os_ = ev_cache(7, small, 0)
+    pos, off = F.random_playouts(2, 300, mode=N.PLAYOUT_PLIES, threads=8)
+    kids = [F.game_children(g["position"], g["moves"]) for g in GAMES[:4]]
+    cpos = np.concatenate([k[0] for k in kids])
+    coff = np.concatenate([[0]] + [k[1][1:] + sum(len(x[0]) for x in kids[:i]) for i, k in enumerate(kids)])
+    for p, o, mode in ((pos, off, N.GROUP_CHAIN), (cpos, coff.astype(np.uint32), N.GROUP_STAR)):
+        ps, po, ps2, po2 = eb.eval_groups_dual(es, p, o, mode)
+        a, b = eb.eval_groups(p, o, mode)
+        c, d = es.eval_groups(p, o, mode)
+        assert np.array_equal(ps, a) and np.array_equal(po, b), mode
+        assert np.array_equal(ps2, c) and np.array_equal(po2, d), mode
+        for on, x, y in ((ob, ps, po), (os_, ps2, po2)):
+            ops, opo, rc = on.eval_packed(p, threads=8)
+            assert rc == 0 and np.array_equal(x, ops) and np.array_equal(y, opo), mode
+    if big == 1024:
+        pos, off = F.random_playouts(11, 14_000, max_plies=160, mode=N.PLAYOUT_PLIES, threads=16)
+        assert len(pos) > (1 << 20)
+        ps, po, ps2, po2 = eb.eval_groups_dual(es, pos, off, N.GROUP_CHAIN)
+        a, b = eb.eval_groups(pos, off, N.GROUP_CHAIN)
+        c, d = es.eval_groups(pos, off, N.GROUP_CHAIN)
+        assert np.array_equal(ps, a) and np.array_equal(po, b) and np.array_equal(ps2, c) and np.array_equal(po2, d)
+        idx = np.r_[0:2000, (1 << 20) - 2000:(1 << 20) + 2000]
+        ops, opo, rc = os_.eval_packed(pos[idx], threads=8)
+        assert np.array_equal(ps2[idx], ops) and np.array_equal(po2[idx], opo)
+
+
+def test_dual_groups_rejects_mismatched_contexts(ev_cache):
+    eb, _ = ev_cache(1, 1024, 0)
+    pos, off = F.random_playouts(2, 10, mode=N.PLAYOUT_PLIES, threads=2)
+    with pytest.raises(F.FnnueError) as e:
+        eb.eval_groups_dual(eb, pos, off)
+    assert e.value.name == "FNNUE_E_ARG"
+    zh = F.Evaluator(F.Net.from_bytes_variant(F.synthesize_variant_net(5, 256, N.VARIANT_CRAZYHOUSE),
+                                              N.VARIANT_CRAZYHOUSE), 0)
+    try:
+        with pytest.raises(F.FnnueError) as e:
+            eb.eval_groups_dual(zh, pos, off)
+        assert e.value.name == "FNNUE_E_ARCH"
+    finally:
+        zh.close()
+
+
 def test_children_star(ev_cache):
     ev, on = ev_cache()
     for g in GAMES[:3]:

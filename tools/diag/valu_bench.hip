@@ -30,6 +30,21 @@ KERNEL(k_pkmul, "v_pk_mul_lo_u16 %0, %0, %1")
 KERNEL(k_and_or, "v_and_or_b32 %0, %0, %1, %2")
 KERNEL(k_mov, "v_mov_b32 %0, %1")
 
+// 64-bit SWAR candidate: one v_lshl_add_u64 adds four
+// int16 columns held as one 64-bit word (shift 0), vs two v_add_u32.
+#define OP64(INSN, r) asm volatile(INSN : "+v"(r) : "v"(b64));
+#define BODY64(INSN) \
+  OP64(INSN, a0) OP64(INSN, a1) OP64(INSN, a2) OP64(INSN, a3) OP64(INSN, a4) OP64(INSN, a5) OP64(INSN, a6) OP64(INSN, a7)
+#define KERNEL64(NAME, INSN)                                                                        \
+  __global__ void NAME(unsigned* out, int iters) {                                                  \
+    unsigned long long a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,        \
+                       a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;                                       \
+    const unsigned long long b64 = ((unsigned long long)blockIdx.x << 32) | threadIdx.x;            \
+    for (int i = 0; i < iters; ++i) { BODY64(INSN) BODY64(INSN) }                                   \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
+  }
+KERNEL64(k_lshladd64, "v_lshl_add_u64 %0, %0, 0, %1")
+
 int main() {
   int cus = 0;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -40,7 +55,8 @@ int main() {
   K ks[] = {{"v_add_u32", k_add}, {"v_add3_u32", k_add3}, {"v_pk_add_u16", k_pkadd}, {"v_add_u32_sdwa", k_sdwa},
             {"v_mad_u32_u16", k_mad16}, {"v_lshl_add_u32", k_lshladd}, {"v_bfe_u32", k_bfe}, {"v_perm_b32", k_perm},
             {"v_pk_max_i16", k_pkmax}, {"v_pk_mul_lo_u16", k_pkmul}, 
-            {"v_and_or_b32", k_and_or}, {"v_mov_b32", k_mov}};
+            {"v_and_or_b32", k_and_or}, {"v_mov_b32", k_mov},
+            {"v_lshl_add_u64", k_lshladd64}};
   for (int wps : {2, 4, 8}) {  // waves per SIMD: wps/4 1024-thread WGs per CU (or one WG of 256*wps)
   printf("--- %d waves per SIMD\n", wps);
   const dim3 grid(wps <= 4 ? cus : cus * (wps / 4)), block(wps <= 4 ? 256 * wps : 1024);

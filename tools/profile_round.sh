@@ -6,7 +6,9 @@
 #   pmc_<k>/ one PMC pass per counter set, each its own run (never combined
 #            with tracing domains; every set within the per-block limits)
 # then tools/roofline.py turns them into gpurun_out/prof_<tag>/counters.json.
-#   usage: tools/profile_round.sh <tag> [workload ...]   (default: all three)
+#   usage: tools/profile_round.sh <tag> [workload ...]   (default: all of them)
+# A workload "<name>@<hd>" profiles bench.py --workload <name> --hd <hd>
+# (counters keyed so; bench.py reads them for that width, e.g. the small net).
 set -uo pipefail
 TAG=${1:-rXX}; shift || true
 WLS=${*:-positions games children crazyhouse atomic crazyhouse-games atomic-games}
@@ -20,7 +22,8 @@ SETS=(
   "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"
 )
 for wl in $WLS; do
-  args="--workload $wl"
+  args="--workload ${wl%@*}"
+  [[ $wl == *@* ]] && args="$args --hd ${wl#*@}"
   D=$OUT/$wl
   mkdir -p "$D"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- \
