@@ -163,6 +163,15 @@ struct SegCtr {
 // the offsets (non-decreasing, off[0] = 0, off[ngroups] = npos; else error bit
 // 2, FNNUE_E_ARG): the offsets of a *_device call never come to the host.
 // span == nullptr: check only (the gather path).
+// A group longer than kSpanChunk (one long CHAIN, or a whole batch sent as one
+// group) is not filled by its one wave, which would walk it serially (ADVICE
+// r03): the wave fills it up to the next kSpanChunk-aligned position and
+// writes the span at every aligned position inside it; group_span_big_kernel
+// (one workgroup per aligned chunk of positions) then fills the rest of each
+// chunk whose first entry names such a group.  Every aligned position's entry
+// is written by the first kernel (by its small group, or as a big group's
+// marker), so the second kernel never reads a stale entry.
+constexpr uint32_t kSpanChunk = 4096;
 __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
                                                          uint32_t npos, uint2* __restrict__ span, int check,
                                                          uint32_t* __restrict__ err) {
@@ -175,7 +184,23 @@ __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restr
   }
   if (!span) return;
   const uint32_t a = min(off[g], npos), b = min(max(off[g + 1], a), npos);
-  for (uint32_t i = a + (threadIdx.x & 63); i < b; i += 64) span[i] = make_uint2(a, b);
+  const uint2 v = make_uint2(a, b);
+  const uint32_t lane = threadIdx.x & 63;
+  if (b - a <= kSpanChunk) {
+    for (uint32_t i = a + lane; i < b; i += 64) span[i] = v;
+    return;
+  }
+  const uint32_t a1 = (a + kSpanChunk - 1) / kSpanChunk * kSpanChunk;  // < b: the group is longer than a chunk
+  for (uint32_t i = a + lane; i < a1; i += 64) span[i] = v;
+  for (uint32_t i = a1 + lane * kSpanChunk; i < b; i += 64 * kSpanChunk) span[i] = v;
+}
+
+__global__ __launch_bounds__(256) void group_span_big_kernel(uint32_t npos, uint2* __restrict__ span) {
+  const uint32_t c0 = blockIdx.x * kSpanChunk;
+  const uint2 v = span[c0];
+  if (v.y - v.x <= kSpanChunk) return;  // a small group's entry: the chunk is filled
+  const uint32_t e = min(c0 + kSpanChunk, min(v.y, npos));
+  for (uint32_t i = c0 + 1 + threadIdx.x; i < e; i += 256) span[i] = v;
 }
 
 // The group of chunk position i (absolute position sbase + i), in chunk
@@ -482,30 +507,35 @@ __global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Po
   __shared__ uint32_t lbase[kIB];
   __shared__ uint32_t lists[1024 * kListStrideWords];  // list staging, one row per lane
   const uint32_t K = cref[2 * n], K0 = cref[n];
-  if (blockIdx.x * blockDim.x >= K) return;  // workgroup-uniform
-  for (int i = threadIdx.x; i < kIB; i += blockDim.x) lcnt[i] = 0;
-  __syncthreads();
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t c = k >= K0 ? 1u : 0u, i = k < K ? ipos[k] : 0u;
-  const uint32_t L = k < K ? len[c * n + i] : 0u;
-  const bool live = L != 0;
-  typename Fs::Dec d;
-  uint32_t key = 0, rk = 0;
-  if (live) {
-    d = Fs::decode(pos + i);
-    key = seg_key<Fs>(d, (int)c, L);
-    rk = atomicAdd(&lcnt[key], 1u);
+  // Grid-stride over 1024-item blocks: the item count is known only here, and
+  // a grid sized for 2n items launched mostly empty 103-KB workgroups.
+  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < K; b0 += gridDim.x * blockDim.x) {
+    __syncthreads();  // the previous block's LDS counts are read
+    for (int i = threadIdx.x; i < kIB; i += blockDim.x) lcnt[i] = 0;
+    __syncthreads();
+    const uint32_t k = b0 + threadIdx.x;
+    const uint32_t c = k >= K0 ? 1u : 0u, i = k < K ? ipos[k] : 0u;
+    const uint32_t L = k < K ? len[c * n + i] : 0u;
+    const bool live = L != 0;
+    typename Fs::Dec d;
+    uint32_t key = 0, rk = 0;
+    if (live) {
+      d = Fs::decode(pos + i);
+      key = seg_key<Fs>(d, (int)c, L);
+      rk = atomicAdd(&lcnt[key], 1u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < kIB; t += blockDim.x)
+      lbase[t] = lcnt[t] ? atomicAdd(&ctr[SegCtr<Fs>::kCur + t], lcnt[t]) : 0;
+    __syncthreads();
+    if (live) {
+      const uint32_t slot = lbase[key] + rk;
+      const uint32_t half = d.b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(d.b.cnt - 1) >> 2;
+      items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)d.nfeat);
+      const uint32_t pp = (slot - ctr[SegCtr<Fs>::kOff + (key / SegCtr<Fs>::kNB) * SegCtr<Fs>::kNB]) & 1u;  // parity in its king block
+      Fs::write_list(d, (int)c, slot, pp, lists + threadIdx.x * kListStrideWords, flist);
+    }
   }
-  __syncthreads();
-  for (int t = threadIdx.x; t < kIB; t += blockDim.x)
-    lbase[t] = lcnt[t] ? atomicAdd(&ctr[SegCtr<Fs>::kCur + t], lcnt[t]) : 0;
-  __syncthreads();
-  if (!live) return;
-  const uint32_t slot = lbase[key] + rk;
-  const uint32_t half = d.b.stm == (int)c ? 0u : 1u, bk = (uint32_t)(d.b.cnt - 1) >> 2;
-  items[slot] = make_uint4(i | half << 24 | bk << 25, L, c, (uint32_t)d.nfeat);
-  const uint32_t pp = (slot - ctr[SegCtr<Fs>::kOff + (key / SegCtr<Fs>::kNB) * SegCtr<Fs>::kNB]) & 1u;  // parity in its king block
-  Fs::write_list(d, (int)c, slot, pp, lists + threadIdx.x * kListStrideWords, flist);
 }
 
 struct SegFetch {
@@ -868,7 +898,7 @@ hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, 
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL((plan_scan_kernel_t<Fs::KB, SegCtr<Fs>::kNB>), dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(seg_scatter_kernel<Fs>, dim3((2 * n + 1023) / 1024), dim3(1024), 0, stream, pos, n, G.cref,
+  hipLaunchKernelGGL(seg_scatter_kernel<Fs>, dim3(min((2 * n + 1023) / 1024, 512u)), dim3(1024), 0, stream, pos, n, G.cref,
                      G.ipos, G.len, P.ctr, (uint4*)G.items, P.flist);
   return hipGetLastError();
 }
@@ -909,6 +939,10 @@ hipError_t launch_group_span(const uint32_t* off, uint32_t ngroups, uint32_t npo
   if (ngroups == 0) return hipSuccess;
   hipLaunchKernelGGL(group_span_kernel, dim3((ngroups + 3) / 4), dim3(256), 0, stream, off, ngroups, npos,
                      static_cast<uint2*>(span), check ? 1 : 0, err);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !span || npos == 0) return e;
+  hipLaunchKernelGGL(group_span_big_kernel, dim3((npos + kSpanChunk - 1) / kSpanChunk), dim3(256), 0, stream, npos,
+                     static_cast<uint2*>(span));
   return hipGetLastError();
 }
 

@@ -269,6 +269,26 @@ def test_full_size_properties(ev_cache):
     assert np.array_equal(ps2[1::2], ps[:200_000]) and np.array_equal(po2[1::2], po[:200_000])
 
 
+def test_groups_longer_than_a_span_chunk(ev_cache):
+    """Groups longer than the 4096-position span chunk (one CHAIN over a whole
+    random game corpus, a single group holding every position of the call,
+    mixed with small and empty groups) give the from-scratch
+    results: grouping never changes a result, and the span table of a long
+    group is filled by one workgroup per chunk."""
+    ev, on = ev_cache()
+    pos, off = F.random_playouts(21, 4000, mode=N.PLAYOUT_PLIES, threads=8)
+    ps, po = ev.eval_positions(pos)
+    n = len(pos)
+    cuts = [0, 4095, 4095, 4096 * 3 + 17, 4096 * 3 + 18, 4096 * 5, 4096 * 5 + 4097, n - 3, n]
+    for o in (np.array([0, n], np.uint32), np.array(cuts, np.uint32)):
+        for mode in (N.GROUP_CHAIN, N.GROUP_STAR):
+            gs, go = ev.eval_groups(pos, o, mode)
+            assert np.array_equal(gs, ps) and np.array_equal(go, po), (len(o), mode)
+    idx = np.arange(0, n, 97)
+    ops, opo, rc = on.eval_packed(pos[idx], threads=8)
+    assert np.array_equal(ps[idx], ops) and np.array_equal(po[idx], opo)
+
+
 def test_image_broadcast_path(ev_cache):
     """ctx from a device image (what bench.py broadcasts over RCCL) == ctx from the net."""
     import torch
