@@ -59,3 +59,36 @@ def test_analysis_json_capacity():
     buf = C.create_string_buffer(4)
     rc = N.lib.fnnue_backend_analysis_json(arr, 1, buf, len(buf), C.byref(n))
     assert rc == -10 and n.value > 4
+
+
+def test_game_end_known_positions():
+    """fnnue_game_end (host replay): what the engine answers with mate 0 /
+    cp 0 and bestmove (none) ([ref] src/stockfish.rs:359-376)."""
+    import fishnet_amd as F
+    assert F.game_end(START, "f2f3 e7e5 g2g4 d8h4") == F.END_NO_MOVES | F.END_CHECK  # fool's mate
+    assert F.game_end("7k/5Q2/5K2/8/8/8/8/8 w - - 0 1", "f6g6") == F.END_NO_MOVES  # stalemate
+    assert F.game_end(START, "e2e4 e7e5 d1h5 b8c6") == 0
+    assert F.game_end(START, "e2e4 e7e5 d1h5 g7g6 h5e5") == F.END_CHECK  # check, not mate
+    # atomic: Nxf7 explodes the black king on e8; the game is over there
+    assert F.game_end(START, "g1f3 e7e6 f3g5 f8e7 g5f7", N.VARIANT_ATOMIC) == F.END_NO_MOVES | F.END_EXTINCT
+    # crazyhouse: a back-rank mate by a drop (black has nothing in hand to block)
+    zh = "7k/6pp/8/8/8/8/8/K7[R] w - - 0 1"
+    assert F.game_end(zh, "R@e8", N.VARIANT_CRAZYHOUSE) == F.END_NO_MOVES | F.END_CHECK
+    assert F.game_end("7k/6pp/8/8/8/8/8/K7[Rr] w - - 0 1", "R@e8", N.VARIANT_CRAZYHOUSE) == F.END_CHECK  # r@f8 blocks
+    with pytest.raises(N.FnnueError) as e:
+        F.game_end(START, "e2e5")
+    assert e.value.name == "FNNUE_E_MOVE"
+
+
+def test_channel_nets_slot_checks_without_a_device():
+    """fnnue_backend_channel_nets refuses a net in the wrong slot (and no net
+    at all) before it touches a device."""
+    import ctypes as C
+    import fishnet_amd as F
+    chess = F.Net.from_bytes(F.synthesize_net(1, 128))
+    zh = F.Net.from_bytes_variant(F.synthesize_variant_net(2, 256, N.VARIANT_CRAZYHOUSE), N.VARIANT_CRAZYHOUSE)
+    h = C.c_void_p()
+    for nets, code in (((None, None, None), -1), ((zh._h, None, None), -4), ((None, chess._h, None), -4),
+                       ((None, None, zh._h), -4)):
+        rc = N.lib.fnnue_backend_channel_nets(C.byref(B._Nets(*nets)), 0, None, C.byref(h))
+        assert rc == code, (nets, rc)

@@ -177,3 +177,25 @@ def test_variant_golden_vectors():
         assert rc == 0
         digest = hashlib.sha256(wps.astype("<i4").tobytes() + wpo.astype("<i4").tobytes()).hexdigest()
         assert digest == e["walks_sha256"]
+
+
+def test_variant_oracle_atomic_game_over_record():
+    """An atomic position with one king exploded is a game-over record: the
+    oracle answers (0, 0) without an error (the evaluator does the same on the
+    GPU); no king at all, or a missing crazyhouse king, stays invalid."""
+    import fishnet_amd as F
+    from oracle.oracle import VariantOracleNet
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    pos = F.game_vpositions(ATOMIC, start, "g1f3 e7e6 f3g5 f8e7 g5f7")
+    on = VariantOracleNet(F.synthesize_variant_net(3, 256, ATOMIC), ATOMIC)
+    ps, po, rc = on.eval_packed(pos)
+    assert rc == 0 and ps[-1] == 0 and po[-1] == 0 and np.any(po[:-1])
+    gps, gpo, grc = on.eval_groups(pos, np.array([0, len(pos)], np.uint32), 0)
+    assert grc == 0 and np.array_equal(gps, ps) and np.array_equal(gpo, po)
+    bad = pos[-1:].copy()
+    bad[0, :32] &= np.where((bad[0, :32] & 15) == 6, 0xF0, 0xFF).astype(np.uint8)
+    bad[0, :32] &= np.where((bad[0, :32] >> 4) == 6, 0x0F, 0xFF).astype(np.uint8)
+    assert on.eval_packed(bad)[2] != 0
+    onz = VariantOracleNet(F.synthesize_variant_net(3, 256, CZH), CZH)
+    zpos = pos[-1:].copy()
+    assert onz.eval_packed(zpos)[2] != 0

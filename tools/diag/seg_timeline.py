@@ -99,6 +99,10 @@ def main():
         ov = np.clip(np.minimum(end, b) - np.maximum(start, a), 0, None).sum()
         occ.append(round(float(ov / (b - a) / len(ucu)), 3))
     res["cu_occupancy_by_time"] = occ
+    S = args.hd // 64
+    sl = live % S
+    res["task_us_by_slice"] = {"slice0": round(float(dur[sl == 0].mean()) / 1e3, 2),
+                               "others": round(float(dur[sl != 0].mean()) / 1e3, 2)}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     json.dump(res, open(args.out, "w"), indent=1)
     print(json.dumps(res))
