@@ -10,9 +10,14 @@
 #   4. the bench lines of every workload carry counters.tree_matches = true.
 # Everything lands in gpurun_out/<tag>/ (copy counters.json back into
 # profiles/ on the build machine).
-#   usage: tools/final_round.sh <tag> [skip-tests]
+#   usage: tools/final_round.sh <tag> [phase ...]   phases: tests profile bench (default: all)
+# (one gpurun call may last 20 minutes: run the phases in two calls if needed;
+# the bench phase installs the profile phase's counters first)
 set -uo pipefail
 tag=${1:-rXX}
+shift || true
+phases=${*:-tests profile bench}
+has() { [[ " $phases " == *" $1 "* ]]; }
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
@@ -24,13 +29,19 @@ step() {  # step <name> <timeout_s> <cmd...>
   tail -n 2 "$out/$name.log" | cut -c1-300
   if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
-if [ "${2:-}" != "skip-tests" ]; then
+if has tests; then
   step gputest 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
-step profile 1800 bash tools/profile_round.sh "$tag" positions games children crazyhouse atomic crazyhouse-games \
-  atomic-games games@128 positions@128
-step install 120 python tools/roofline.py "gpurun_out/prof_$tag" --install
+if has profile; then
+  step profile 1800 bash tools/profile_round.sh "$tag" positions games children crazyhouse atomic crazyhouse-games \
+    atomic-games games@128 positions@128
+fi
+has bench || exit 0
+# counters of this call's profile phase; in a call of its own the bench phase
+# uses the profiles/counters.json installed from them on the build machine
+# (gpurun_out/ does not travel to the next box)
+[ -d "gpurun_out/prof_$tag" ] && step install 120 python tools/roofline.py "gpurun_out/prof_$tag" --install
 cp profiles/counters.json "$out/counters.json"
 b() {  # b <name> <bench args...>
   local name=$1; shift
