@@ -603,17 +603,11 @@ __device__ __forceinline__ int32_t psqt_delta(const int32_t* ptile, const uint4&
   return (int32_t)(p(d.z & 0xFFFFu) + a2 - p(d.y & 0xFFFFu) - p(d.y >> 16));
 }
 
-// One pass = 8 segment items per wave.  kCols: the pass's column slice —
-// refresh position as slice_pass (ft_sliced.hip), then the wave walks the
-// longest segment of the pass; finished items turn their rows into the zero
-// row and their stores out of range (dropped).  kPsqt: the PSQT part (every
-// bucket, one per lane q of the item, because the bucket changes along a
-// segment), on column slice 0 or, for nets of at most 2 slices, as a task of
-// its own per unit without a tile: there slice 0 is half of the launch's tasks
-// and, carrying the PSQT sums too, takes ~1.5-2x the others — the span of a
-// launch that is one round of tasks (HD 128: ft_segments 0.149 -> 0.116-0.121
-// ms on config 3).  For the big nets the separate task costs more than it
-// balances (HD 1024: 0.432 -> 0.581 ms; profiles/r04/ab_psqt_task.txt).
+// One pass = 8 segment items per wave.  Refresh position: as slice_pass
+// (ft_sliced.hip) but the PSQT sum keeps all 8 buckets, one per lane q of the
+// item, because the bucket changes along a segment (kPsqt: slice 0 only).
+// Then the wave walks the longest segment of the pass; finished items turn
+// their rows into the zero row and their stores out of range (dropped).
 constexpr int kDbufStride = 9;  // records per item in the per-wave LDS buffer (8 + 1 padding)
 // One LDS buffer per wave serves both the pass's feature lists (64 x 8 B) and
 // the walk's delta records (8 items x kDbufStride x 16 B): a wave uses them
@@ -624,7 +618,7 @@ constexpr int kWaveBufU4 = 8 * kDbufStride;
 typedef uint2 lds_u2 __attribute__((may_alias));
 typedef uint4 lds_u4 __attribute__((may_alias));
 
-template <int HD, bool kStar, bool kCols, bool kPsqt, bool kSwar, uint32_t kNone>
+template <int HD, bool kStar, bool kPsqt, bool kSwar, uint32_t kNone>
 __device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ wbuf, int lane, int it_in_wave, int s,
                                          int q, uint32_t n, const char* lbase, u16x4 b_lo, u16x4 b_hi, int krow,
                                          const int32_t* ptile, __amdgpu_buffer_rsrc_t psqt_rsrc,
@@ -645,12 +639,10 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ 
     e[4 * m + 3] = v.w;
   }
   u16x4 lo = b_lo, hi = b_hi;
+  rows_sum<kSwar>((int)maxn - 1, e, lbase, lo, hi);
   const uint32_t col = 32 * s + 4 * q;
-  if constexpr (kCols) {
-    rows_sum<kSwar>((int)maxn - 1, e, lbase, lo, hi);
-    __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc,
-                                          ((rec.x & kSlotMask) * 2 + ((rec.x >> 24) & 1)) * (HD / 2) + col, 0, 0);
-  }
+  __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc,
+                                        ((rec.x & kSlotMask) * 2 + ((rec.x >> 24) & 1)) * (HD / 2) + col, 0, 0);
   int32_t p = 0;
   auto psqt_off = [&](uint32_t x, bool live) {
     return (live && (int)(x >> 25) == q) ? ((x & kSlotMask) * 2 + ((x >> 24) & 1)) * 4u : kDroppedOffset;
@@ -704,12 +696,9 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ 
     for (int jj = 0; jj < 8; ++jj) {
       if (kLast && jj > 0 && (uint32_t)jj >= rest) break;
       const uint4 d = db[jj];  // past the segment's end: the sentinel record (seg_place_kernel)
-      if constexpr (kCols) {
-        apply_delta<kAdd2, kSwar>(lbase, d, blo, bhi, lo, hi);
-        const uint32_t xo = (d.x & kRowMask) * (HD / 2) + col;
-        __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc, xo, 0,
-                                              0);
-      }
+      apply_delta<kAdd2, kSwar>(lbase, d, blo, bhi, lo, hi);
+      const uint32_t xo = (d.x & kRowMask) * (HD / 2) + col;
+      __builtin_amdgcn_raw_buffer_store_b32(kSwar ? transform4_swar(lo, hi) : transform4(lo, hi), x_rsrc, xo, 0, 0);
       int32_t pc = 0;
       if constexpr (kPsqt) {
         pc = (int32_t)((uint32_t)pb + (uint32_t)psqt_delta<kAdd2>(ptile, d, q));
@@ -757,8 +746,6 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
                                                            int32_t* __restrict__ psqt_part,
                                                            uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
-  constexpr bool kSepPsqt = S <= 2;               // the PSQT part as a task of its own (see seg_pass)
-  constexpr int kTasks = S + (kSepPsqt ? 1 : 0);  // per unit: S column slices [, then its PSQT task]
   using G = typename Fs::G;
   constexpr int kTileU4 = G::kTileU4;
   __shared__ uint4 img[kTileU4];
@@ -788,38 +775,30 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   const __amdgpu_buffer_rsrc_t drec_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n + 16), kBufferFlags);
   uint4* wb = wbufs[wv];
-  // Grid-stride over (unit, task) pairs: the unit count is known only on the
+  // Grid-stride over (unit, slice) pairs: the unit count is known only on the
   // device and its bound (seg_max_units) is far above typical counts.  The
-  // grid is a multiple of 8 * kTasks, so every pair keeps its XCD-aware
-  // mapping (all tasks of a unit on one XCD: its lists and records are read
-  // into one L2).  Task s < S: column slice s (slice 0 with the PSQT part
-  // unless kSepPsqt); s == S: the PSQT part.
+  // grid is a multiple of 8 * S, so every pair keeps its XCD-aware mapping.
   const uint32_t nunits = ctr[SegCtr<Fs>::kNUnits];
   for (uint32_t w = blockIdx.x;; w += gridDim.x) {
     const uint32_t j = w >> 3;
-    const uint32_t unit = (j / kTasks) * 8 + (w & 7);
-    const int s = (int)(j % kTasks);
-    const bool psqt_task = kSepPsqt && s == S;
-    const bool psqt_here = kSepPsqt ? psqt_task : s == 0;  // this task sums the PSQT part
+    const uint32_t unit = (j / S) * 8 + (w & 7);
+    const int s = (int)(j % S);
     if (unit >= nunits) return;
     __syncthreads();  // the previous unit's tile reads are done before the reload
     if (threadIdx.x == 0) claim = 16;
     const int4 u = units[unit];
-    const int sc = psqt_task ? 0 : s;  // column slice (the PSQT task reads no tile)
-    const uint4* src = tiles + ((size_t)u.x * S + sc) * kTileU4;
+    const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
     uint4 t[kTileLoads];
-    if (!psqt_task) {
 #pragma unroll
-      for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
-    }
+    for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
     uint4 pt[2];
     const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * G::kRows * kPsqtBuckets);
-    if (psqt_here) {
+    if (s == 0) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
     }
-    u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * sc + 4 * q);
-    u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * sc + 4 * q);
+    u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
+    u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
     const int krow = G::king_row(u.x);
     const char* lbase = reinterpret_cast<const char*>(img) + G::kPlaneBytes * q;
     const int last = u.z - 1;
@@ -831,16 +810,14 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
     int kp = wv;
     int base = pass_base(kp);
     SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
-    if (!psqt_task) {
 #pragma unroll
-      for (int k = 0; k < kTileLoads; ++k)
-        if ((int)threadIdx.x + 1024 * k < kTileU4) {
-          uint4 v = t[k];
-          if constexpr (kSwar) v = swar_tile_words(v);
-          img[threadIdx.x + 1024 * k] = v;
-        }
-    }
-    if (psqt_here) {
+    for (int k = 0; k < kTileLoads; ++k)
+      if ((int)threadIdx.x + 1024 * k < kTileU4) {
+        uint4 v = t[k];
+        if constexpr (kSwar) v = swar_tile_words(v);
+        img[threadIdx.x + 1024 * k] = v;
+      }
+    if (s == 0) {
       uint4* pdst = reinterpret_cast<uint4*>(ptile);
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -868,15 +845,12 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
       kp = __builtin_amdgcn_readfirstlane((int)c);
       const int next = pass_base(kp);
       fa = fetch_seg(items_rsrc, flist_rsrc, next, last, lane, it_in_wave);
-      if (psqt_task)
-        seg_pass<HD, kStar, false, true, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi,
-                                                           krow, ptile, psqt_rsrc, x_rsrc, drec_rsrc);
-      else if (!kSepPsqt && s == 0)
-        seg_pass<HD, kStar, true, true, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi,
-                                                          krow, ptile, psqt_rsrc, x_rsrc, drec_rsrc);
+      if (s == 0)
+        seg_pass<HD, kStar, true, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
+                                                    ptile, psqt_rsrc, x_rsrc, drec_rsrc);
       else
-        seg_pass<HD, kStar, true, false, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi,
-                                                           krow, ptile, psqt_rsrc, x_rsrc, drec_rsrc);
+        seg_pass<HD, kStar, false, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
+                                                     ptile, psqt_rsrc, x_rsrc, drec_rsrc);
       base = next;
     }
   }
@@ -885,11 +859,11 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
 template <int HD, class Fs>
 hipError_t ft_segments_t(const SegPlan& G, const SlicedPlan& P, const NetPtrs& net, uint32_t n, bool star,
                          uint8_t* x, uint32_t max_units, hipStream_t stream) {
-  constexpr int kTasks = HD / 64 + (HD / 64 <= 2 ? 1 : 0);  // the kernel's kTasks
-  // grid = 8 * kTasks * G (see the kernel's grid stride); up to 8 * 64 units per sweep
+  constexpr int S = HD / 64;
+  // grid = 8 * S * G (see the kernel's grid stride); up to 8 * 64 units per sweep
   const uint32_t groups = min((max_units + 7) / 8, 64u);
   auto launch = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(groups * 8 * kTasks), dim3(1024), 0, stream, (const uint4*)P.tiles, net.ft_bias, P.ctr,
+    hipLaunchKernelGGL(kern, dim3(groups * 8 * S), dim3(1024), 0, stream, (const uint4*)P.tiles, net.ft_bias, P.ctr,
                        (const int4*)P.units, (const uint4*)G.items, P.flist, (const uint4*)G.drec, n, net.psqt_w,
                        P.psqt_part, x);
   };
