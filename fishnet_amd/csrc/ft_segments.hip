@@ -734,6 +734,128 @@ __device__ __forceinline__ void seg_pass(const SegFetch& f, uint4* __restrict__ 
   }
 }
 
+// One net's view for a (unit, slice) task: its LDS-tile image, bias, PSQT
+// rows, and the buffer resources of its PSQT parts and x (the plan's items,
+// lists and delta records are the same for every net of the feature set).
+struct SegNet {
+  const uint4* tiles;
+  const int16_t* ftb;
+  const int32_t* psqw;
+  __amdgpu_buffer_rsrc_t psqt_rsrc, x_rsrc;
+};
+
+// Buffer ranges are the launch's exact extents (x: n rows of HD bytes, < 2^31;
+// psqt_part: 2n words; drec: 2n + 1 records, the last the sentinel record 2n).
+// Items past their segment's end read the sentinel, whose x row 2n and PSQT
+// word 2n fall just past the x and psqt_part ranges, so the hardware drops
+// those stores; other dropped stores use kDroppedOffset.  No record can reach
+// beyond the launch's rows.
+template <int HD>
+__device__ __forceinline__ SegNet seg_net(const uint4* tiles, const int16_t* ftb, const int32_t* psqw,
+                                          int32_t* psqt_part, uint8_t* x, uint32_t n) {
+  return SegNet{tiles, ftb, psqw, __builtin_amdgcn_make_buffer_rsrc(psqt_part, 0, (int)(8 * n), kBufferFlags),
+                __builtin_amdgcn_make_buffer_rsrc(x, 0, (int)min((uint64_t)n * HD, (uint64_t)kBufferRange),
+                                                  kBufferFlags)};
+}
+
+// The LDS a task works in (declared by the kernel): the tile, the PSQT tile,
+// one buffer per wave (a pass's lists, then its delta records) and the pass
+// counter.
+template <class Fs>
+struct SegLds {
+  uint4 img[Fs::G::kTileU4];
+  int32_t ptile[Fs::G::kTileRows * kPsqtBuckets];
+  uint4 wbufs[16][kWaveBufU4];
+  uint32_t claim;  // next pass of the unit to hand out
+};
+
+// Column slice s (of the net's HD / 64) of `unit`: the tile to LDS, the own
+// king into the bias, then the unit's passes, claimed longest first.
+template <int HD, bool kStar, bool kSwar, class Fs>
+__device__ __forceinline__ void seg_task(SegLds<Fs>& L, const SegNet& net, int s, const int4 u, uint32_t n,
+                                         __amdgpu_buffer_rsrc_t items_rsrc, __amdgpu_buffer_rsrc_t flist_rsrc,
+                                         __amdgpu_buffer_rsrc_t drec_rsrc) {
+  constexpr int S = HD / 64;
+  using G = typename Fs::G;
+  constexpr int kTileU4 = G::kTileU4;
+  constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
+  constexpr int kPtileU4 = G::kTileRows * kPsqtBuckets / 4, kPtileRealU4 = G::kRows * kPsqtBuckets / 4;
+  static_assert(kPtileU4 <= 2048, "PSQT tile loads: two per thread");
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int it_in_wave, q;
+  lane_item(lane, it_in_wave, q);
+  uint4* wb = L.wbufs[wv];
+  __syncthreads();  // the previous unit's tile reads are done before the reload
+  if (threadIdx.x == 0) L.claim = 16;
+  const uint4* src = net.tiles + ((size_t)u.x * S + s) * kTileU4;
+  uint4 t[kTileLoads];
+#pragma unroll
+  for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
+  uint4 pt[2];
+  const uint4* psrc = reinterpret_cast<const uint4*>(net.psqw + (size_t)u.x * G::kRows * kPsqtBuckets);
+  if (s == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
+  }
+  u16x4 b_lo = *reinterpret_cast<const u16x4*>(net.ftb + 32 * s + 4 * q);
+  u16x4 b_hi = *reinterpret_cast<const u16x4*>(net.ftb + HD / 2 + 32 * s + 4 * q);
+  const int krow = G::king_row(u.x);
+  const char* lbase = reinterpret_cast<const char*>(L.img) + G::kPlaneBytes * q;
+  const int last = u.z - 1;
+  // Passes are handed out longest first (items are sorted by length bin, so
+  // from the unit's end backwards), the next one claimed from an LDS counter
+  // when the current one starts: waves finish within one pass of each other.
+  const int npass = (u.z - u.y + 7) / 8;
+  auto pass_base = [&](int k) { return k < npass ? u.y + (npass - 1 - k) * 8 : (int)u.z; };
+  int kp = wv;
+  int base = pass_base(kp);
+  SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
+#pragma unroll
+  for (int k = 0; k < kTileLoads; ++k)
+    if ((int)threadIdx.x + 1024 * k < kTileU4) {
+      uint4 v = t[k];
+      if constexpr (kSwar) v = swar_tile_words(v);
+      L.img[threadIdx.x + 1024 * k] = v;
+    }
+  if (s == 0) {
+    uint4* pdst = reinterpret_cast<uint4*>(L.ptile);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = (int)threadIdx.x + 1024 * k;
+      if (i < kPtileU4) pdst[i] = i < kPtileRealU4 ? pt[k] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  {  // the own-king row (every item of the unit has it) joins the bias
+    const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
+    if constexpr (kSwar) {
+      b_lo = swar_words(b_lo);
+      b_hi = swar_words_hi(b_hi);
+    }
+    accum_row<kSwar>(kv, b_lo, b_hi);
+    if constexpr (kSwar) {  // both halves of every word offset by 0x8000 (transform4_swar)
+      b_lo = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_lo) + kSwarOffset);
+      b_hi = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_hi) + kSwarOffset);
+    }
+  }
+  while (base < u.z) {
+    const SegFetch cur = fa;
+    uint32_t c = 0;
+    if (lane == 0) c = atomicAdd(&L.claim, 1u);
+    kp = __builtin_amdgcn_readfirstlane((int)c);
+    const int next = pass_base(kp);
+    fa = fetch_seg(items_rsrc, flist_rsrc, next, last, lane, it_in_wave);
+    if (s == 0)
+      seg_pass<HD, kStar, true, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
+                                                  L.ptile, net.psqt_rsrc, net.x_rsrc, drec_rsrc);
+    else
+      seg_pass<HD, kStar, false, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
+                                                   L.ptile, net.psqt_rsrc, net.x_rsrc, drec_rsrc);
+    base = next;
+  }
+}
+
 template <int HD, bool kStar, bool kSwar, class Fs>
 __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restrict__ tiles,
                                                            const int16_t* __restrict__ ftb,
@@ -746,35 +868,14 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
                                                            int32_t* __restrict__ psqt_part,
                                                            uint8_t* __restrict__ x) {
   constexpr int S = HD / 64;
-  using G = typename Fs::G;
-  constexpr int kTileU4 = G::kTileU4;
-  __shared__ uint4 img[kTileU4];
-  __shared__ int32_t ptile[G::kTileRows * kPsqtBuckets];
-  __shared__ uint4 wbufs[16][kWaveBufU4];  // per wave: a pass's lists, then its delta records
-  __shared__ uint32_t claim;  // next pass of the unit to hand out
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int it_in_wave, q;
-  lane_item(lane, it_in_wave, q);
-  constexpr int kTileLoads = (kTileU4 + 1023) / 1024;
-  constexpr int kPtileU4 = G::kTileRows * kPsqtBuckets / 4, kPtileRealU4 = G::kRows * kPsqtBuckets / 4;
-  static_assert(kPtileU4 <= 2048, "PSQT tile loads: two per thread");
-  // Buffer ranges are this launch's exact extents (x: n rows of HD bytes,
-  // < 2^31; psqt_part: 2n words; drec: 2n + 1 records, the last the sentinel
-  // record 2n).  Items past their segment's end read the sentinel, whose x row
-  // 2n and PSQT word 2n fall just past the x and psqt_part ranges, so the
-  // hardware drops those stores; other dropped stores use kDroppedOffset.  No
-  // record can reach beyond the launch's rows.
-  const __amdgpu_buffer_rsrc_t psqt_rsrc = __builtin_amdgcn_make_buffer_rsrc(psqt_part, 0, (int)(8 * n), kBufferFlags);
-  const __amdgpu_buffer_rsrc_t x_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(x, 0, (int)min((uint64_t)n * HD, (uint64_t)kBufferRange), kBufferFlags);
+  __shared__ SegLds<Fs> L;
+  const SegNet net = seg_net<HD>(tiles, ftb, psqw, psqt_part, x, n);
   const __amdgpu_buffer_rsrc_t items_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(items), 0, kBufferAll, kBufferFlags);
   const __amdgpu_buffer_rsrc_t flist_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(flist), 0, kBufferAll, kBufferFlags);
   const __amdgpu_buffer_rsrc_t drec_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(drec), 0, (int)(32 * n + 16), kBufferFlags);
-  uint4* wb = wbufs[wv];
   // Grid-stride over (unit, slice) pairs: the unit count is known only on the
   // device and its bound (seg_max_units) is far above typical counts.  The
   // grid is a multiple of 8 * S, so every pair keeps its XCD-aware mapping.
@@ -782,77 +883,8 @@ __global__ __launch_bounds__(1024) void ft_segments_kernel(const uint4* __restri
   for (uint32_t w = blockIdx.x;; w += gridDim.x) {
     const uint32_t j = w >> 3;
     const uint32_t unit = (j / S) * 8 + (w & 7);
-    const int s = (int)(j % S);
     if (unit >= nunits) return;
-    __syncthreads();  // the previous unit's tile reads are done before the reload
-    if (threadIdx.x == 0) claim = 16;
-    const int4 u = units[unit];
-    const uint4* src = tiles + ((size_t)u.x * S + s) * kTileU4;
-    uint4 t[kTileLoads];
-#pragma unroll
-    for (int k = 0; k < kTileLoads; ++k) t[k] = src[min((int)threadIdx.x + 1024 * k, kTileU4 - 1)];
-    uint4 pt[2];
-    const uint4* psrc = reinterpret_cast<const uint4*>(psqw + (size_t)u.x * G::kRows * kPsqtBuckets);
-    if (s == 0) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) pt[k] = psrc[min((int)threadIdx.x + 1024 * k, kPtileRealU4 - 1)];
-    }
-    u16x4 b_lo = *reinterpret_cast<const u16x4*>(ftb + 32 * s + 4 * q);
-    u16x4 b_hi = *reinterpret_cast<const u16x4*>(ftb + HD / 2 + 32 * s + 4 * q);
-    const int krow = G::king_row(u.x);
-    const char* lbase = reinterpret_cast<const char*>(img) + G::kPlaneBytes * q;
-    const int last = u.z - 1;
-    // Passes are handed out longest first (items are sorted by length bin, so
-    // from the unit's end backwards), the next one claimed from an LDS counter
-    // when the current one starts: waves finish within one pass of each other.
-    const int npass = (u.z - u.y + 7) / 8;
-    auto pass_base = [&](int k) { return k < npass ? u.y + (npass - 1 - k) * 8 : (int)u.z; };
-    int kp = wv;
-    int base = pass_base(kp);
-    SegFetch fa = fetch_seg(items_rsrc, flist_rsrc, base, last, lane, it_in_wave);
-#pragma unroll
-    for (int k = 0; k < kTileLoads; ++k)
-      if ((int)threadIdx.x + 1024 * k < kTileU4) {
-        uint4 v = t[k];
-        if constexpr (kSwar) v = swar_tile_words(v);
-        img[threadIdx.x + 1024 * k] = v;
-      }
-    if (s == 0) {
-      uint4* pdst = reinterpret_cast<uint4*>(ptile);
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int i = (int)threadIdx.x + 1024 * k;
-        if (i < kPtileU4) pdst[i] = i < kPtileRealU4 ? pt[k] : make_uint4(0, 0, 0, 0);
-      }
-    }
-    __syncthreads();
-    {  // the own-king row (every item of the unit has it) joins the bias
-      const u32x4 kv = *reinterpret_cast<const u32x4*>(lbase + 16 * krow);
-      if constexpr (kSwar) {
-        b_lo = swar_words(b_lo);
-        b_hi = swar_words_hi(b_hi);
-      }
-      accum_row<kSwar>(kv, b_lo, b_hi);
-      if constexpr (kSwar) {  // both halves of every word offset by 0x8000 (transform4_swar)
-        b_lo = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_lo) + kSwarOffset);
-        b_hi = __builtin_bit_cast(u16x4, __builtin_bit_cast(u32x2, b_hi) + kSwarOffset);
-      }
-    }
-    while (base < u.z) {
-      const SegFetch cur = fa;
-      uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(&claim, 1u);
-      kp = __builtin_amdgcn_readfirstlane((int)c);
-      const int next = pass_base(kp);
-      fa = fetch_seg(items_rsrc, flist_rsrc, next, last, lane, it_in_wave);
-      if (s == 0)
-        seg_pass<HD, kStar, true, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
-                                                    ptile, psqt_rsrc, x_rsrc, drec_rsrc);
-      else
-        seg_pass<HD, kStar, false, kSwar, Fs::kNone>(cur, wb, lane, it_in_wave, s, q, n, lbase, b_lo, b_hi, krow,
-                                                     ptile, psqt_rsrc, x_rsrc, drec_rsrc);
-      base = next;
-    }
+    seg_task<HD, kStar, kSwar, Fs>(L, net, (int)(j % S), units[unit], n, items_rsrc, flist_rsrc, drec_rsrc);
   }
 }
 
