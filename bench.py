@@ -683,7 +683,7 @@ def main():
                                  "counters": {"source": db.get("source"), "tree_matches": tree_ok,
                                               "key": f"{args.workload}@{args.small_net}"}}
         small["how"] = ("one fnnue_eval_groups_dual_device call per step: one plan, the small net's FT + stacks on "
-                        "the small context's stream beside the big net's stacks" if dual else
+                        "the small context's stream beside the big net's FT and stacks" if dual else
                         "a second evaluation call per step on the small net's context")
 
     if rank == 0:
