@@ -244,7 +244,17 @@ __global__ __launch_bounds__(256) void ft_groups_kernel(const fnnue_pos* __restr
   const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   const u16 b_lo = u16::load(net.ft_bias, lane), b_hi = u16::load(net.ft_bias + HD / 2, lane);
-  for (uint32_t g = wid; g < ngroups; g += nw) {
+  // The groups overlapping [lo, hi): from the first one ending after lo to
+  // the last one starting before hi (offsets are non-decreasing; group_span's
+  // check fails a call whose offsets are not), so a launch walks its chunk's
+  // groups only, not all of them.
+  uint32_t g0 = 0;
+  for (uint32_t top = ngroups; g0 < top;) {
+    const uint32_t m = (g0 + top) / 2;
+    if (off[m + 1] <= lo) g0 = m + 1;
+    else top = m;
+  }
+  for (uint32_t g = g0 + wid; g < ngroups && off[g] < hi; g += nw) {
     // the group clamped to this launch's positions [lo, hi) (a group cut at lo
     // restarts there with a refresh; malformed offsets give empty ranges)
     const uint32_t begin = max(off[g], lo), end = min(off[g + 1], hi);
@@ -572,7 +582,9 @@ hipError_t launch_groups_t(const fnnue_pos* pos, const uint32_t* off, uint32_t n
                            int mode,
                            const NetPtrs& net, uint8_t* x, int32_t* psqt, uint8_t* bucket, uint32_t* err,
                            hipStream_t stream) {
-  uint32_t blocks = (ngroups + 3) / 4;
+  // one wave per group of the chunk (about hi - lo positions' worth at most,
+  // empty groups aside: the waves grid-stride)
+  uint32_t blocks = std::min((ngroups + 3) / 4, (hi - lo + 3) / 4 + 1);
   if (blocks > 8192) blocks = 8192;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((ft_groups_kernel<HD, 4>), dim3(blocks), dim3(256), 0, stream, pos, off, ngroups, lo, hi,

@@ -116,6 +116,27 @@ def test_chunk_boundary_wide_net(ev_cache):
     assert np.array_equal(gs[idx], ops) and np.array_equal(go[idx], opo)
 
 
+def test_gather_groups_across_chunks(ev_cache):
+    """The per-group gather kernel walks only the groups overlapping its
+    chunk (a binary search over the offsets): CHAIN groups across the HD-3072
+    chunk boundary, with empty groups mixed in (repeated offsets), equal the
+    segment path everywhere and the oracle around the boundary."""
+    ev, on = ev_cache(*WIDE[2])
+    chunk = min(1 << 20, (0x7FFFFFFF // 3072) & ~1023)
+    gpos, off = F.random_playouts(33, 9000, mode=N.PLAYOUT_PLIES, threads=8)
+    assert off[-1] > chunk
+    off = np.sort(np.concatenate([off, off[::97], off[::1000]])).astype(np.uint32)
+    res = []
+    for impl in (N.FT_SLICED, N.FT_GATHER):
+        ev.set_ft_impl(impl)
+        res.append(ev.eval_groups(gpos, off, N.GROUP_CHAIN))
+    ev.set_ft_impl(N.FT_SLICED)
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
+    idx = np.r_[0:1000, chunk - 2000:chunk + 2000, len(gpos) - 1000:len(gpos)]
+    ops, opo, rc = on.eval_packed(gpos[idx], threads=8)
+    assert np.array_equal(res[1][0][idx], ops) and np.array_equal(res[1][1][idx], opo)
+
+
 def test_same_king_block_everywhere(ev_cache):
     """Degenerate plan: every item in one king block / one n bin (one huge bin,
     many units for a single tile)."""
