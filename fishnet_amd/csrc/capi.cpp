@@ -281,6 +281,7 @@ int next_events(fnnue_ctx* c, std::array<hipEvent_t, 4>** out) {
 
 int ensure_seg(fnnue_ctx* c) {
   SegPlan& G = c->seg;
+  G.unit_plies = seg_unit_plies(c->hd);
   if (G.ref) return FNNUE_OK;
   const size_t n2 = 2 * (size_t)c->chunk;
   G.scan_temp_bytes = seg_scan_temp_bytes(c->chunk);

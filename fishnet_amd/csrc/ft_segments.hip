@@ -928,7 +928,8 @@ hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, 
   hipLaunchKernelGGL(seg_place_kernel<Fs>, dim3(cb), dim3(1024), 0, stream, n, sp, sbase, star ? 1 : 0, bucket, G.ref,
                      G.cref, G.ipos, G.len, (const uint4*)G.dtmp, (uint4*)G.drec, P.ctr);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL((plan_scan_kernel_t<Fs::KB, SegCtr<Fs>::kNB>), dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u);
+  hipLaunchKernelGGL((plan_scan_kernel_t<Fs::KB, SegCtr<Fs>::kNB>), dim3(1), dim3(1024), 0, stream, P.ctr, (int4*)P.units, 0u,
+                     G.unit_plies);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(seg_scatter_kernel<Fs>, dim3(min((2 * n + 1023) / 1024, 512u)), dim3(1024), 0, stream, pos, n, G.cref,
                      G.ipos, G.len, P.ctr, (uint4*)G.items, P.flist);
@@ -937,13 +938,15 @@ hipError_t seg_plan_t(const typename Fs::Pos* pos, uint32_t n, const uint2* sp, 
 
 }  // namespace
 
-// units close at kSegUnitPlies of work, an item weighing at most
+// units close at unit_plies of work, an item weighing at most
 // seg_bin_weight(32): a unit holding fewer than kSegUnitPlies / that many items
 // is its king block's last
-uint32_t seg_max_units(uint32_t chunk) {
-  constexpr uint32_t per = kSegUnitPlies / seg_bin_weight(32);
+uint32_t seg_max_units(uint32_t chunk, uint32_t unit_plies) {
+  const uint32_t per = (unit_plies ? unit_plies : std::min(kSegUnitPlies, kSegUnitPliesSmall)) / seg_bin_weight(32);
   return 64 + (2 * chunk + per - 1) / per;
 }
+
+uint32_t seg_unit_plies(uint32_t hd) { return seg_unit_plies_for(hd); }
 
 size_t seg_ctr_words() {
   return std::max({SegCtr<ChessFs>::kWords, SegCtr<VariantFs<kVariantCrazyhouse>>::kWords,
@@ -997,7 +1000,7 @@ hipError_t launch_seg_ft(uint32_t hd, int variant, uint32_t n, int mode, const N
                          const SegPlan& G, uint8_t* x, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const bool star = mode == FNNUE_GROUP_STAR;
-  const uint32_t mu = seg_max_units(n);
+  const uint32_t mu = seg_max_units(n, G.unit_plies);
   if (variant == kVariantChess) {
 #define CALL(H) ft_segments_t<H, ChessFs>(G, P, net, n, star, x, mu, stream)
     FNNUE_HD_DISPATCH(hd, CALL)

@@ -108,10 +108,14 @@ struct SegPlan {
   size_t span_cap;
   void* scan_temp;
   size_t scan_temp_bytes;
+  uint32_t unit_plies;  // work per segment unit (seg_unit_plies_for the planning net's HD)
 };
 size_t seg_scan_temp_bytes(uint32_t chunk);
 size_t seg_ctr_words();  // counter words of the segment plans (any feature set)
-uint32_t seg_max_units(uint32_t chunk);  // unit-table entries ft_segments may need
+// unit-table entries ft_segments may need for units of unit_plies (0: the
+// smallest units any net uses, for sizing)
+uint32_t seg_max_units(uint32_t chunk, uint32_t unit_plies = 0);
+uint32_t seg_unit_plies(uint32_t hd);  // the segment unit size of a net of width hd
 // Once per grouped call: span[i] = {first, end} of position i's group
 // (absolute, npos entries; span == nullptr: check only).  check: the offsets
 // are checked on the device (non-decreasing, spanning [0, npos)), latching

@@ -159,21 +159,31 @@ __host__ __device__ constexpr uint32_t seg_len_bin(uint32_t L) {
 // kSegUnitPlies of work (items are sorted by length bin).  An item costs its
 // root refresh plus one delta step per further position: the refresh sums the
 // root's whole list (~25 rows, ~100 VALU per lane against ~27 for a delta
-// position), so an item may weigh kSegRootCost + the bin's longest length.
-// Counting positions alone (kSegRootCost 0) makes units of short segments
+// position), so an item weighs kSegRootCost + the bin's longest length.
+// Counting positions alone (kSegRootCost 0) made units of short segments
 // (king moves, STAR children that move the king: one refresh each) up to 3-6x
 // the work of the others (task timeline, tools/diag/seg_timeline.py,
 // profiles/r04g); weighing the refresh (4) evens the tasks out (longest 152 ->
-// 71 us on config 3) but not the kernel time: those long tasks start early and
-// the span is the total work plus one average task (A/B in profiles/r04h:
-// neutral on games, -2 % on children), so the default stays 0.
+// 71 us on config 3): config 3 1163M -> 1179M, config 4 1115M -> 1164M
+// (profiles/r04q; an earlier A/B that called it neutral compared two identical
+// builds, see tools/exp_build.sh).
 #ifndef SEG_UNIT_PLIES
 #define SEG_UNIT_PLIES 16384
 #endif
+#ifndef SEG_UNIT_PLIES_SMALL
+#define SEG_UNIT_PLIES_SMALL 8192
+#endif
 #ifndef SEG_ROOT_COST
-#define SEG_ROOT_COST 0
+#define SEG_ROOT_COST 4
 #endif
 constexpr uint32_t kSegUnitPlies = SEG_UNIT_PLIES;
+// Nets of at most 4 column slices (HD <= 256) get units of half the work: 2
+// slices per unit leave ~250 tasks for 256 CUs at 16384, one round whose span
+// is its longest task (config 3 at HD 128: ft_segments 0.144 -> 0.094 ms).
+constexpr uint32_t kSegUnitPliesSmall = SEG_UNIT_PLIES_SMALL;
+__host__ __device__ constexpr uint32_t seg_unit_plies_for(uint32_t hd) {
+  return hd <= 256 ? kSegUnitPliesSmall : kSegUnitPlies;
+}
 constexpr uint32_t kSegRootCost = SEG_ROOT_COST;
 __host__ __device__ constexpr uint32_t seg_bin_longest(uint32_t bin) {
   return bin < 16 ? bin + 1 : bin < 32 ? 8 * bin - 104 : 160;
@@ -190,7 +200,7 @@ __host__ __device__ constexpr uint32_t seg_count_class(uint32_t nfeat) {
 }
 
 // One workgroup of 1024 threads.  unit_items = 0: segment units (see
-// kSegUnitPlies) instead of fixed-size ones.  KB king blocks (32: chess; 64:
+// seg_plies of work) instead of fixed-size ones.  KB king blocks (32: chess; 64:
 // the variant feature sets), counters laid out as KB * NB item bins + 9
 // position bins, then offsets, cursors and the unit count (kCnt / kOff / kCur
 // / kNUnits for KB = 32, kV* for 64, SegCtr for segments).  NB = 33: bin =
@@ -198,7 +208,8 @@ __host__ __device__ constexpr uint32_t seg_count_class(uint32_t nfeat) {
 template <int KB, int NB = 33>
 __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel_t(uint32_t* __restrict__ ctr,
                                                                                   int4* __restrict__ units,
-                                                                                  uint32_t unit_items) {
+                                                                                  uint32_t unit_items,
+                                                                                  uint32_t seg_plies = 0) {
   constexpr int kIB = KB * NB, kB = kIB + kPosBins, kO = kB, kC = 2 * kB, kNU = 3 * kB;
   auto len_bin = [](int i) { return (i % NB) / (NB / 33); };
   __shared__ uint32_t s[kB];
@@ -248,7 +259,7 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
   if (unit_items == 0) {
     // Segment units: unit u of king block kb starts at the first item whose
     // cumulative work (a bin's items weighed seg_bin_weight) reaches
-    // u * kSegUnitPlies.  Bins are contiguous in item order, so each
+    // u * seg_plies.  Bins are contiguous in item order, so each
     // (kb, bin) thread places the unit starts falling inside its bin.
     __shared__ uint32_t pb[kIB];        // positions before bin i within its king block
     __shared__ uint32_t ubase[KB + 1];  // first unit of each king block
@@ -264,7 +275,7 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
         pb[t * NB + b] = run;
         run += v;
       }
-      const uint32_t mine = (run + kSegUnitPlies - 1) / kSegUnitPlies;
+      const uint32_t mine = (run + seg_plies - 1) / seg_plies;
       uint32_t incl = mine;
 #pragma unroll
       for (int o = 1; o < KB; o <<= 1) {
@@ -283,8 +294,8 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
       if (i >= kIB || local[k] == 0) continue;
       const int kb = i / NB;
       const uint32_t w = seg_bin_weight(len_bin(i)), p0 = pb[i], p1 = p0 + local[k] * w;
-      for (uint32_t u = (p0 + kSegUnitPlies - 1) / kSegUnitPlies; u * kSegUnitPlies < p1; ++u)
-        units[ubase[kb] + u] = make_int4(kb, (int)(s[i] + (u * kSegUnitPlies - p0 + w - 1) / w), 0, 0);
+      for (uint32_t u = (p0 + seg_plies - 1) / seg_plies; u * seg_plies < p1; ++u)
+        units[ubase[kb] + u] = make_int4(kb, (int)(s[i] + (u * seg_plies - p0 + w - 1) / w), 0, 0);
     }
     __syncthreads();  // the starts are visible to the whole workgroup
     // Ends: the next unit's start, or the block's end.  Only .z is written

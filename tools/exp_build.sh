@@ -18,6 +18,9 @@ make -s -C "$ROOT/fishnet_amd/csrc" -j8 ARCH=gfx950 >/dev/null
 cp -a "$ROOT/fishnet_amd/csrc" "$W/fishnet_amd/csrc"
 cp -a "$ROOT/include" "$W/include"
 if [ -n "$patch" ]; then sleep 1; (cd "$W" && patch -p1 --quiet < "$patch"); fi
+# -D flags change every object: make cannot see them, so nothing may be reused
+# (until round 4 a flags-only build silently reused the main objects)
+if [ $# -gt 0 ]; then rm -rf "$W/fishnet_amd/csrc/build" "$W/fishnet_amd/libfnnue.so"; fi
 make -s -C "$W/fishnet_amd/csrc" -j8 ARCH=gfx950 HIPFLAGS="--offload-arch=gfx950 --offload-compress $*" >/dev/null
 cp "$W/fishnet_amd/libfnnue.so" "$ROOT/exp/libfnnue_$name.so"
 echo "exp/libfnnue_$name.so"
