@@ -168,7 +168,7 @@ __host__ __device__ constexpr uint32_t seg_len_bin(uint32_t L) {
 // (profiles/r04q; an earlier A/B that called it neutral compared two identical
 // builds, see tools/exp_build.sh).
 #ifndef SEG_UNIT_PLIES
-#define SEG_UNIT_PLIES 20480
+#define SEG_UNIT_PLIES 16384
 #endif
 #ifndef SEG_UNIT_PLIES_SMALL
 #define SEG_UNIT_PLIES_SMALL 8192
@@ -180,8 +180,6 @@ constexpr uint32_t kSegUnitPlies = SEG_UNIT_PLIES;
 // Nets of at most 4 column slices (HD <= 256) get units of half the work: 2
 // slices per unit leave ~250 tasks for 256 CUs at 16384, one round whose span
 // is its longest task (config 3 at HD 128: ft_segments 0.144 -> 0.094 ms).
-// (Big nets: 20480 against 16384 / 12288: config 3 +0.9 % / -1.9 %, config
-// 4 ±0 / -0.5 %, profiles/r04n.)
 constexpr uint32_t kSegUnitPliesSmall = SEG_UNIT_PLIES_SMALL;
 __host__ __device__ constexpr uint32_t seg_unit_plies_for(uint32_t hd) {
   return hd <= 256 ? kSegUnitPliesSmall : kSegUnitPlies;
@@ -484,11 +482,10 @@ __device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word
 }
 
 #ifndef FT_DEPTH
-#define FT_DEPTH 2
+#define FT_DEPTH 3
 #endif
 // Rows in flight per wave: the LDS queue stays fed and hipcc counts lgkmcnt
-// instead of draining it (2 against 3: config 2 +0.2 %, config 3 +0.5 %;
-// 4: -0.4 % / -5 %, profiles/r04n).
+// instead of draining it.
 constexpr int kRowDepth = 4 * FT_DEPTH;
 
 // SWAR rows (ft_slices when the net allows it, accumulator_bound in net.h):
