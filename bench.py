@@ -30,6 +30,9 @@ Other workloads (the other BASELINE configs, measured for DESIGN.md):
   --workload crazyhouse-games / atomic-games
                        config 5 along games: every ply of 10k random legal variant games per GPU
                        (drops, pockets, explosions), incremental CHAIN (fnnue_eval_vgroups_device)
+  --workload backend   the drop-in itself: lichess-shaped acquired analysis batches (FEN + UCI moves,
+                       40-160 plies, some chess960 / crazyhouse / atomic) through fnnue_backend_go at
+                       --go-batches per call (host text in, responses out: the component fishnet calls)
 
 roofline: the binding resource of the dominant kernel (ft_slices for config
 2, ft_segments for configs 3/4) from the committed PMC profile of this tree
@@ -70,7 +73,11 @@ def parse_args():
                     help="timed steps (1000: ~1.5 s of config 2, long enough for an SMI sampler to see the GPU busy)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic", "crazyhouse-games",
-                                           "atomic-games"], default="positions")
+                                           "atomic-games", "backend"], default="positions")
+    ap.add_argument("--go-batches", default="1,64,1024,16384",
+                    help="backend workload: acquired batches per fnnue_backend_go call (comma list; the value is the "
+                         "largest)")
+    ap.add_argument("--go-seconds", type=float, default=1.5, help="backend workload: timed wall per batch count")
     ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions / variant workloads)")
     ap.add_argument("--games", type=int, default=None,
                     help="games per GPU (games: 10,000 = config 3; children: 5,000 ~ 12.5M positions per GPU = "
@@ -230,8 +237,170 @@ def make_inputs(F, args, seed, threads):
     return pos, off
 
 
+def chess960_fen(rng) -> str:
+    """A Chess960 start position (Shredder-FEN castling letters)."""
+    back = [""] * 8
+    back[int(rng.choice([0, 2, 4, 6]))] = "b"
+    back[int(rng.choice([1, 3, 5, 7]))] = "b"
+    for pc in ("q", "n", "n"):
+        free = [i for i in range(8) if not back[i]]
+        back[int(rng.choice(free))] = pc
+    free = [i for i in range(8) if not back[i]]
+    for i, pc in zip(free, "rkr"):
+        back[i] = pc
+    rooks = [chr(ord("a") + i) for i in free[::2]]
+    castle = "".join(r.upper() for r in rooks[::-1]) + "".join(rooks[::-1])
+    return f"{''.join(back)}/pppppppp/8/8/8/8/PPPPPPPP/{''.join(back).upper()} w {castle} - 0 1"
+
+
+def lichess_batches(F, seed: int, count: int, c960: float = 0.05, variants: float = 0.04):
+    """Acquired analysis batches shaped like lichess work ([ref] src/api.rs:293-309,
+    src/stats.rs:136-138: ~60 positions per batch): a root FEN and 40-160
+    random legal UCI moves; standard chess, a share of Chess960 starts and of
+    crazyhouse / atomic games (seeded)."""
+    from fishnet_amd import backend as B
+    rng = np.random.default_rng(seed)
+    start = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"
+    bodies = []
+    for i in range(count):
+        plies = int(rng.integers(40, 161))
+        u = float(rng.random())
+        if u < variants:
+            zh = u < variants / 2
+            fen = start.replace(" w", "[] w") if zh else start
+            name = "crazyhouse" if zh else "atomic"
+            mv = F.random_vgame(seed * 1_000_003 + i, F.VARIANT_CRAZYHOUSE if zh else F.VARIANT_ATOMIC, fen, plies)
+            bodies.append(B.AcquireResponseBody(f"b{i}", fen, mv, variant=name))
+        elif u < variants + c960:
+            fen = chess960_fen(rng)
+            bodies.append(B.AcquireResponseBody(f"b{i}", fen, F.random_game(seed * 1_000_003 + i, fen, plies),
+                                                variant="chess960"))
+        else:
+            bodies.append(B.AcquireResponseBody(f"b{i}", start, F.random_game(seed * 1_000_003 + i, start, plies)))
+    return bodies
+
+
+def main_backend(args):
+    """The drop-in as fishnet would call it: fnnue_backend_go over acquired
+    analysis batches (host text in, PositionResponses out, one call = one
+    step), at several batch counts per call; the CPU baseline expands and
+    evaluates the same chess batches on every usable core."""
+    import ctypes as C
+
+    import torch
+
+    import fishnet_amd as F
+    from fishnet_amd import _native as N
+    from fishnet_amd import backend as B
+
+    if args.gpus != 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--workload backend runs one actor on one GPU (the reference runs one engine per worker)")
+    cpus = host_cpus()
+    threads = args.threads or cpus["usable"]
+    sizes = sorted({int(x) for x in args.go_batches.split(",") if x.strip()})
+    t0 = time.time()
+    chess_net = F.synthesize_net(args.seed, args.hd, 0)
+    zh_net = F.synthesize_variant_net(args.seed + 5, 512, F.VARIANT_CRAZYHOUSE)
+    at_net = F.synthesize_variant_net(args.seed + 6, 512, F.VARIANT_ATOMIC)
+    stub, actor = B.channel(F.Net.from_bytes(chess_net), 0,
+                            crazyhouse=F.Net.from_bytes_variant(zh_net, F.VARIANT_CRAZYHOUSE),
+                            atomic=F.Net.from_bytes_variant(at_net, F.VARIANT_ATOMIC))
+    t_net = time.time() - t0
+    t0 = time.time()
+    bodies = lichess_batches(F, args.seed, max(sizes))
+    arr, keep = B._acquired(bodies)
+    plies = np.array([B.batch_size(b) for b in bodies], dtype=np.int64)
+    cap = int(plies.sum())
+    out = (B._Response * cap)()
+    off = np.zeros(len(bodies) + 1, dtype=np.uint32)
+    rc = np.zeros(len(bodies), dtype=np.int32)
+    t_gen = time.time() - t0
+    h = actor._h
+
+    def go(k):
+        N.check(N.lib.fnnue_backend_go(h, arr, k, out, cap, N.ptr(off), N.ptr(rc)))
+
+    rows = []
+    for k in sizes:
+        npk = int(plies[:k].sum())
+        for _ in range(max(args.warmup, 1)):
+            go(k)
+        # reps from one probe call: about --go-seconds of wall per batch count
+        tp = time.perf_counter()
+        go(k)
+        probe = time.perf_counter() - tp
+        reps = int(min(2000, max(args.steps if args.steps < 1000 else 3, args.go_seconds / max(probe, 1e-6))))
+        times = []
+        for _ in range(reps):
+            tp = time.perf_counter()
+            go(k)
+            times.append(time.perf_counter() - tp)
+        t = np.array(times)
+        assert not rc[:k].any(), "a synthetic batch failed"
+        rows.append({"batches_per_go": k, "positions_per_go": npk, "calls": reps,
+                     "ms_per_go_mean": round(float(t.mean()) * 1e3, 4),
+                     "ms_per_go_median": round(float(np.median(t)) * 1e3, 4),
+                     "ms_per_go_min": round(float(t.min()) * 1e3, 4),
+                     "positions_per_s": npk / float(t.mean())})
+    top = rows[-1]
+    kmax = top["batches_per_go"]
+    # results of the last (largest) call: parity spot check + CPU baseline on the chess batches
+    got_ps = np.array([out[i].psqt for i in range(int(off[kmax]))], dtype=np.int32)
+    got_po = np.array([out[i].positional for i in range(int(off[kmax]))], dtype=np.int32)
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        from oracle.oracle import OracleNet  # cpu_baseline leg (test infrastructure)
+        from oracle.oracle import lib as olib
+        chess = [i for i in range(kmax) if bodies[i].variant in ("standard", "chess960")]
+        games = [(bodies[i].position, bodies[i].moves) for i in chess]
+        text, fo, mo = F.pack_games(games)
+        oo = np.concatenate([[0], np.cumsum(plies[chess])]).astype(np.uint32)
+        on = OracleNet(chess_net)
+        done, t_cpu = 0, time.perf_counter()
+        first = None
+        while True:
+            ps, po, crc = on.simd_eval_games(text, fo, mo, oo, threads=threads)
+            assert crc == 0
+            first = first or (ps, po)
+            done += int(oo[-1])
+            if time.perf_counter() - t_cpu >= args.cpu_seconds:
+                break
+        cpu_el = time.perf_counter() - t_cpu
+        isa = "AVX-512 VNNI" if olib.cpu_simd_isa512() else "AVX2"
+        cpu = {"value": done / cpu_el, "unit": "positions/s", "cores": threads, "kind": "port",
+               "cpu": {k: cpus[k] for k in ("model", "os_cpu_count", "affinity", "cgroup_quota", "omp_num_threads")},
+               "sample": f"the {len(chess)} chess batches ({int(oo[-1])} plies) of the largest call, repeated for "
+                         f"{cpu_el:.1f} s on {threads} threads: FEN parse + UCI replay + every ply evaluated along "
+                         f"the game (oracle/nnue_cpu_simd.c cpu_simd_eval_games, Stockfish's {isa} NNUE code paths "
+                         f"restated; variant batches excluded: no Fairy-Stockfish SIMD code exists offline)"}
+        idx = np.concatenate([np.arange(off[i], off[i + 1]) for i in chess]) if chess else np.zeros(0, np.int64)
+        parity = {"checked": int(len(idx)),
+                  "mismatches": int(((got_ps[idx] != first[0]) | (got_po[idx] != first[1])).sum())}
+    actor.close()
+    nvar = sum(1 for b in bodies[:kmax] if b.variant in ("crazyhouse", "atomic"))
+    n960 = sum(1 for b in bodies[:kmax] if b.variant == "chess960")
+    line = {
+        "metric": METRIC, "value": top["positions_per_s"], "unit": "positions/s", "n_gpus": 1,
+        "steps": top["calls"], "warmup": args.warmup, "ms_per_step": top["ms_per_go_mean"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int16", "data": "synthetic",
+        "config": {"workload": f"fnnue_backend_go over lichess-shaped acquired analysis batches (root FEN + 40-160 "
+                               f"random legal UCI moves; {n960} chess960, {nvar} crazyhouse/atomic of {kmax}); "
+                               f"host text in, one PositionResponse per ply out, synthetic nets (chess HD {args.hd}, "
+                               f"variants HD 512)",
+                   "batches_per_go": kmax, "positions_per_go": top["positions_per_go"], "parallelism": "dp1"},
+        "backend": rows,
+        "roofline": None,
+        "cpu_baseline": cpu, "parity_spot_check": parity,
+        "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
+    }
+    del keep
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse_args()
+    if args.workload == "backend":
+        return main_backend(args)
     if args.games is None:
         args.games = 5_000 if args.workload == "children" else 10_000
     import torch

@@ -28,7 +28,9 @@ struct DBoard {
 
 DBoard to_dboard(const Board& b);
 
-constexpr uint32_t kBuildErrFen = 1, kBuildErrMove = 2;
+// kBuildErrCount: a game's move tokens differ from the count its offsets were
+// sized for (the host's count; never for offsets from the builder's own count).
+constexpr uint32_t kBuildErrFen = 1, kBuildErrMove = 2, kBuildErrCount = 3;
 
 // State of a game's last position (optional builder output, one byte per
 // game): a game that ended on the board ends there, since no move can follow.
@@ -44,24 +46,53 @@ struct BuildResult {
   uint32_t err_code = 0, err_game = 0, err_ply = 0;  // kBuildErr*: first failing game, ply (1-based move)
 };
 
+// Grow-only device scratch of the batch builder (one per context, one per
+// backend): per-game ply counts and offsets, the error word, the scan's
+// temporary storage, per-ply boards and children counts.  A steady stream of
+// batches allocates nothing; buffers are freed by release() only.
+struct BuilderScratch {
+  enum { kPlies, kPlyOff, kErr, kScan, kStates, kCnt, kCoff, kSlots };
+  void* p[kSlots] = {};
+  size_t bytes[kSlots] = {};
+  // p[slot] with at least `want` bytes (grows by a quarter beyond the request)
+  hipError_t get(int slot, size_t want, void** out);
+  void release();
+};
+
 // text: game g's FEN in [fen_off[g], mv_off[g]), its space-separated UCI moves
 // in [mv_off[g], fen_off[g + 1]).  children = false: every ply of every game,
 // group g = game g; children = true: one group per ply = the ply's position
 // followed by its legal children (Board::legal_moves order).  d_final
 // (optional, ngames bytes): kFinal* flags of each game's last position.
-// Synchronises `s`.
+// Sizes the outputs on the device and reads the sizes back: synchronises `s`.
 BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
-                               size_t off_cap, hipStream_t s, uint8_t* d_final = nullptr);
+                               size_t off_cap, hipStream_t s, BuilderScratch& ws, uint8_t* d_final = nullptr);
 
-// Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub); synchronises s.
-hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s);
+// Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub, temporary
+// storage from ws); stream-ordered, no host sync.
+hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s, BuilderScratch& ws);
 
 // The same expansion for Fairy-Stockfish variants (vbuilder.hip, vboard.h):
 // crazyhouse / atomic FENs and UCI moves (drops "P@e4"), fnnue_vpos records.
 BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                 uint32_t ngames, bool children, fnnue_vpos* d_out, size_t cap, uint32_t* d_group_off,
-                                size_t off_cap, hipStream_t s, uint8_t* d_final = nullptr);
+                                size_t off_cap, hipStream_t s, BuilderScratch& ws, uint8_t* d_final = nullptr);
+
+// Every ply of every game with offsets the caller already knows (ply_off:
+// ngames + 1 entries, ply_off[g + 1] - ply_off[g] = 1 + the game's move
+// tokens, as fnnue_backend_batch_size counts them): one launch, no sizing
+// pass, no allocation, no host sync.  variant = kVariantChess (d_out:
+// fnnue_pos) or a variant (fnnue_vpos).  d_err: 4 words, zero before the
+// launch; afterwards err[0] = kBuildErr* of a failing game (0: none), err[1]
+// that game, err[2] its ply.  d_final: optional kFinal* per game.
+hipError_t replay_games_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                               const uint32_t* d_ply_off, uint32_t ngames, void* d_out, uint8_t* d_final,
+                               uint32_t* d_err, hipStream_t s);
+// vbuilder.hip's launcher of the same (variants only).
+hipError_t replay_vgames_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                                const uint32_t* d_ply_off, uint32_t ngames, fnnue_vpos* d_out, void* d_states,
+                                uint8_t* d_final, uint32_t* d_err, hipStream_t s);
 
 // Leaf count of perft(depth) summed over the frontier boards (1 <= depth <= 3).
 hipError_t perft_device(const std::vector<DBoard>& frontier, int depth, uint64_t* nodes);

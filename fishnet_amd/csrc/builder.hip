@@ -10,9 +10,10 @@
 // record for record, and fnnue_perft_device pins the move generator on the
 // published perft counts.
 //
-// Work is one thread per game (FEN parse + replay: each ply depends on the
-// previous) and one thread per ply (children).  Boards are bitboards in
-// registers: no tables, attacks from shifts and ray walks.
+// Replay is one 64-lane wave per game (replay_wave.h: the board chain plays a
+// window of moves wave-uniformly, lanes then check the moves and pack the
+// boards in parallel); children are one thread per ply.  Boards are bitboards
+// in registers: no tables, attacks from shifts and ray walks.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -22,6 +23,8 @@
 
 #include "board.h"
 #include "builder.h"
+#include "net.h"
+#include "replay_wave.h"
 
 namespace fnnue {
 
@@ -351,29 +354,10 @@ __device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t en
   return true;
 }
 
-// parse_uci (board.cpp): the legal move whose UCI text, in Chess960
-// (king-takes-rook) or, for standard positions, standard castling notation,
-// equals the token.
-__device__ bool match_uci(const DBoard& b, const char* tok, int len, DMove& out) {
-  if (len != 4 && len != 5) return false;
-  auto sqr = [&](int i) -> int {
-    const char f = tok[i], r = tok[i + 1];
-    return (f >= 'a' && f <= 'h' && r >= '1' && r <= '8') ? (r - '1') * 8 + (f - 'a') : -1;
-  };
-  const int from = sqr(0), to = sqr(2);
-  if (from < 0 || to < 0) return false;
-  int promo = 0;
-  if (len == 5) {
-    switch (tok[4]) {
-      case 'n': promo = KNIGHT; break;
-      case 'b': promo = BISHOP; break;
-      case 'r': promo = ROOK; break;
-      case 'q': promo = QUEEN; break;
-      case 'k': promo = KING; break;
-      case 'p': promo = PAWN; break;
-      default: return false;
-    }
-  }
+// parse_uci (board.cpp) on decoded squares: the legal move from `from` to
+// `to` with promotion `promo` (0 none, KNIGHT..QUEEN), castling written as
+// king-takes-rook or, in standard positions, as the king's two-square step.
+__device__ bool match_decoded(const DBoard& b, int from, int to, int promo, DMove& out) {
   bool found = false;
   for_each_legal(b, [&](const DMove& m) -> bool {
     if (m.from != from || m.promo != promo) return true;
@@ -387,6 +371,104 @@ __device__ bool match_uci(const DBoard& b, const char* tok, int len, DMove& out)
   return found;
 }
 
+// Packed record from the bitboards, branch-free: bit k of a square's nibble
+// is bit k of the piece code (type bits 0-2: P=1 N=2 B=3 R=4 Q=5 K=6; bit 3
+// black), so each nibble plane is an OR of type bitboards, spread from 8 bits
+// of a rank to 8 nibbles.  Equals pack() on every consistent board.
+__device__ __forceinline__ uint32_t spread8(uint32_t x) {
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+
+__device__ fnnue_pos pack_fast(const DBoard& b) {
+  const uint64_t q0 = b.bt[PAWN] | b.bt[BISHOP] | b.bt[QUEEN];
+  const uint64_t q1 = b.bt[KNIGHT] | b.bt[BISHOP] | b.bt[KING];
+  const uint64_t q2 = b.bt[ROOK] | b.bt[QUEEN] | b.bt[KING];
+  const uint64_t q3 = b.bc[BLACK];
+  uint32_t w[9];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const int sh = 8 * r;
+    w[r] = spread8((uint32_t)(q0 >> sh) & 255u) | (spread8((uint32_t)(q1 >> sh) & 255u) << 1) |
+           (spread8((uint32_t)(q2 >> sh) & 255u) << 2) | (spread8((uint32_t)(q3 >> sh) & 255u) << 3);
+  }
+  w[8] = b.stm;
+  fnnue_pos p;
+  memcpy(&p, w, sizeof(p));
+  return p;
+}
+
+// Chess rules of the wave replay (replay_wave.h).
+struct ChessRules {
+  using Board = DBoard;
+  using Move = DMove;
+  using Pos = fnnue_pos;
+  __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int, DBoard& b) {
+    return fnnue::parse_fen(t, p, e, b);
+  }
+  // "e2e4" / "e7e8q" (board.cpp's UCI: lowercase promotion letters n b r q;
+  // 'k' / 'p' or anything else never names a generated move)
+  __device__ static uint32_t encode(const char* c, int len) {
+    const int from = replay::tok_sq(c[0], c[1]), to = replay::tok_sq(c[2], c[3]);
+    if (from < 0 || to < 0) return replay::kTokBad;
+    uint32_t promo = 0;
+    if (len == 5) {
+      switch (c[4]) {
+        case 'n': promo = KNIGHT; break;
+        case 'b': promo = BISHOP; break;
+        case 'r': promo = ROOK; break;
+        case 'q': promo = QUEEN; break;
+        default: return replay::kTokBad;
+      }
+    }
+    return (uint32_t)from | ((uint32_t)to << 6) | (promo << 12);
+  }
+  // The move the code names if it names one: castling when the own king goes
+  // to a castling rook's square or (standard positions) to its two-square
+  // destination; everything else as written (en passant and double pushes
+  // are do_move's business).  verify() decides whether it is legal.
+  __device__ static bool interpret(const DBoard& b, uint32_t code, DMove& m) {
+    const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
+    const uint64_t fm = 1ull << from;
+    if (!(b.bc[b.stm] & fm)) return false;
+    m = DMove{from, to, promo, 0};
+    if ((b.bt[KING] & fm) && !promo) {
+      const int back = b.stm == WHITE ? 0 : 56;
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int rsq = b.cr[b.stm][side];
+        if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
+          m = DMove{from, rsq, 0, 1};
+          return true;
+        }
+      }
+    }
+    return true;
+  }
+  __device__ static void do_move(DBoard& b, const DMove& m) { fnnue::do_move(b, m); }
+  __device__ static bool verify(const DBoard& b, uint32_t code, const DMove& m) {
+    DMove x;
+    return match_decoded(b, (int)replay::tok_from(code), (int)replay::tok_to(code), (int)replay::tok_piece(code), x) &&
+           x.from == m.from && x.to == m.to && x.promo == m.promo && x.castle == m.castle;
+  }
+  __device__ static fnnue_pos pack(const DBoard& b) { return pack_fast(b); }
+  __device__ static bool any_legal_from(const DBoard& b, int sq, bool) {
+    if (!((b.bc[b.stm] >> sq) & 1)) return false;
+    bool any = false;
+    for_each_legal(b, [&](const DMove&) -> bool {
+      any = true;
+      return false;
+    }, 1ull << sq);
+    return any;
+  }
+  __device__ static uint8_t end_flags(const DBoard& b, bool any) {
+    const int k = king_sq(b, b.stm);
+    const bool check = k >= 0 && attacked(b, k, b.stm ^ 1, b.bc[0] | b.bc[1]);
+    return (uint8_t)((any ? 0 : kFinalNoMoves) | (check ? kFinalCheck : 0));
+  }
+};
+
 // ---- kernels ----
 // text layout of game g: FEN in [fen_off[g], mv_off[g]), moves in [mv_off[g], fen_off[g + 1]).
 __global__ void count_plies_kernel(const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
@@ -394,57 +476,6 @@ __global__ void count_plies_kernel(const char* __restrict__ text, const uint32_t
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngames) return;
   plies[g] = 1u + (uint32_t)count_tokens(text, mv_off[g], fen_off[g + 1]);
-}
-
-__device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t game, uint32_t ply) {
-  if (atomicCAS(&err[0], 0u, code) == 0u) {
-    err[1] = game;
-    err[2] = ply;
-  }
-}
-
-// One thread per game: parse, replay, write the position (and, for the
-// children pass, the full state) of every ply.
-__global__ void replay_kernel(const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
-                              const uint32_t* __restrict__ mv_off, uint32_t ngames,
-                              const uint32_t* __restrict__ ply_off, fnnue_pos* __restrict__ out,
-                              DBoard* __restrict__ states, uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngames) return;
-  DBoard b;
-  if (!parse_fen(text, fen_off[g], mv_off[g], b)) {
-    latch(err, kBuildErrFen, g, 0);
-    return;
-  }
-  uint32_t o = ply_off[g];
-  if (out) out[o] = pack(b);
-  if (states) states[o] = b;
-  uint32_t p = mv_off[g], st;
-  const uint32_t end = fen_off[g + 1];
-  uint32_t ply = 0;
-  int len;
-  while ((len = next_token(text, p, end, st)) > 0) {
-    ++ply;
-    DMove m;
-    if (!match_uci(b, text + st, len, m)) {
-      latch(err, kBuildErrMove, g, ply);
-      return;
-    }
-    do_move(b, m);
-    ++o;
-    if (out) out[o] = pack(b);
-    if (states) states[o] = b;
-  }
-  if (final) {
-    bool any = false;
-    for_each_legal(b, [&](const DMove&) -> bool {
-      any = true;
-      return false;
-    });
-    const int k = king_sq(b, b.stm);
-    const bool check = k >= 0 && attacked(b, k, b.stm ^ 1, b.bc[0] | b.bc[1]);
-    final[g] = (uint8_t)((any ? 0 : kFinalNoMoves) | (check ? kFinalCheck : 0));
-  }
 }
 
 __global__ void count_children_kernel(const DBoard* __restrict__ states, uint32_t n, uint32_t* __restrict__ cnt) {
@@ -499,17 +530,36 @@ __global__ void perft_kernel(const DBoard* __restrict__ states, uint32_t n, unsi
 
 }  // namespace
 
+hipError_t BuilderScratch::get(int slot, size_t want, void** out) {
+  if (want > bytes[slot]) {
+    if (p[slot]) (void)hipFree(p[slot]);
+    p[slot] = nullptr;
+    bytes[slot] = 0;
+    const size_t n = want + want / 4 + 256;
+    const hipError_t e = hipMalloc(&p[slot], n);
+    if (e != hipSuccess) return e;
+    bytes[slot] = n;
+  }
+  *out = p[slot];
+  return hipSuccess;
+}
+
+void BuilderScratch::release() {
+  for (int i = 0; i < kSlots; ++i) {
+    if (p[i]) (void)hipFree(p[i]);
+    p[i] = nullptr;
+    bytes[i] = 0;
+  }
+}
+
 // Exclusive scan of cnt[0..n) into off[0..n], off[n] = total (hipcub).
-hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s) {
+hipError_t builder_exclusive_scan(const uint32_t* cnt, uint32_t* off, uint32_t n, hipStream_t s, BuilderScratch& ws) {
   size_t tmp_bytes = 0;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, off, (int)n + 1, s);
   if (e != hipSuccess) return e;
   void* tmp = nullptr;
-  if ((e = hipMalloc(&tmp, tmp_bytes)) != hipSuccess) return e;
-  e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)n + 1, s);
-  const hipError_t e2 = hipStreamSynchronize(s);
-  (void)hipFree(tmp);
-  return e != hipSuccess ? e : e2;
+  if ((e = ws.get(BuilderScratch::kScan, tmp_bytes, &tmp)) != hipSuccess) return e;
+  return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, cnt, off, (int)n + 1, s);
 }
 
 DBoard to_dboard(const Board& h) {
@@ -525,9 +575,32 @@ DBoard to_dboard(const Board& h) {
   return b;
 }
 
+namespace {
+
+hipError_t launch_chess_replay(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                               const uint32_t* d_ply_off, uint32_t ngames, fnnue_pos* d_out, DBoard* d_states,
+                               uint8_t* d_final, uint32_t* d_err, hipStream_t s) {
+  if (!ngames) return hipSuccess;
+  hipLaunchKernelGGL(replay::replay_wave_kernel<ChessRules>, dim3(ngames), dim3(64), 0, s, (int)kVariantChess, d_text,
+                     d_fen_off, d_mv_off, ngames, d_ply_off, d_out, d_states, d_err, d_final);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t replay_games_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                               const uint32_t* d_ply_off, uint32_t ngames, void* d_out, uint8_t* d_final,
+                               uint32_t* d_err, hipStream_t s) {
+  if (variant != kVariantChess)
+    return replay_vgames_device(variant, d_text, d_fen_off, d_mv_off, d_ply_off, ngames,
+                                static_cast<fnnue_vpos*>(d_out), nullptr, d_final, d_err, s);
+  return launch_chess_replay(d_text, d_fen_off, d_mv_off, d_ply_off, ngames, static_cast<fnnue_pos*>(d_out), nullptr,
+                             d_final, d_err, s);
+}
+
 BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                uint32_t ngames, bool children, fnnue_pos* d_out, size_t cap, uint32_t* d_group_off,
-                               size_t off_cap, hipStream_t s, uint8_t* d_final) {
+                               size_t off_cap, hipStream_t s, BuilderScratch& ws, uint8_t* d_final) {
   BuildResult R;
   auto fail = [&](hipError_t e) {
     R.hip = e;
@@ -536,29 +609,20 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
   hipError_t e;
   uint32_t *plies = nullptr, *ply_off = nullptr, *err = nullptr, *cnt = nullptr, *coff = nullptr;
   DBoard* states = nullptr;
-  struct Free {
-    std::vector<void*> p;
-    ~Free() {
-      for (void* x : p) (void)hipFree(x);
-    }
-  } F;
-  auto alloc = [&](void** p, size_t bytes) {
-    hipError_t a = hipMalloc(p, bytes ? bytes : 4);
-    if (a == hipSuccess) F.p.push_back(*p);
-    return a;
-  };
-  if ((e = alloc((void**)&plies, (size_t)(ngames + 1) * 4)) != hipSuccess) return fail(e);
-  if ((e = alloc((void**)&ply_off, (size_t)(ngames + 1) * 4)) != hipSuccess) return fail(e);
-  if ((e = alloc((void**)&err, 16)) != hipSuccess) return fail(e);
+  using W = BuilderScratch;
+  if ((e = ws.get(W::kPlies, (size_t)(ngames + 1) * 4, (void**)&plies)) != hipSuccess) return fail(e);
+  if ((e = ws.get(W::kPlyOff, (size_t)(ngames + 1) * 4, (void**)&ply_off)) != hipSuccess) return fail(e);
+  if ((e = ws.get(W::kErr, 16, (void**)&err)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(err, 0, 16, s)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(plies + ngames, 0, 4, s)) != hipSuccess) return fail(e);
   const uint32_t bs = 64;
   hipLaunchKernelGGL(count_plies_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
                      ngames, plies);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e);
-  if ((e = builder_exclusive_scan(plies, ply_off, ngames, s)) != hipSuccess) return fail(e);
+  if ((e = builder_exclusive_scan(plies, ply_off, ngames, s, ws)) != hipSuccess) return fail(e);
   uint32_t total_plies = 0;
-  if ((e = hipMemcpy(&total_plies, ply_off + ngames, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
+  if ((e = hipMemcpyAsync(&total_plies, ply_off + ngames, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
   if (!children) {
     R.n_out = total_plies;
     R.n_groups = ngames;
@@ -566,19 +630,19 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
       R.capacity = true;
       return R;
     }
-    hipLaunchKernelGGL(replay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
-                       ngames, ply_off, d_out, (DBoard*)nullptr, err, d_final);
-    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = launch_chess_replay(d_text, d_fen_off, d_mv_off, ply_off, ngames, d_out, nullptr, d_final, err, s)) !=
+        hipSuccess)
+      return fail(e);
     if ((e = hipMemcpyAsync(d_group_off, ply_off, (size_t)(ngames + 1) * 4, hipMemcpyDeviceToDevice, s)) !=
         hipSuccess)
       return fail(e);
   } else {
-    if ((e = alloc((void**)&states, (size_t)total_plies * sizeof(DBoard))) != hipSuccess) return fail(e);
-    if ((e = alloc((void**)&cnt, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
-    if ((e = alloc((void**)&coff, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
-    hipLaunchKernelGGL(replay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
-                       ngames, ply_off, (fnnue_pos*)nullptr, states, err, d_final);
-    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = ws.get(W::kStates, (size_t)total_plies * sizeof(DBoard), (void**)&states)) != hipSuccess) return fail(e);
+    if ((e = ws.get(W::kCnt, (size_t)(total_plies + 1) * 4, (void**)&cnt)) != hipSuccess) return fail(e);
+    if ((e = ws.get(W::kCoff, (size_t)(total_plies + 1) * 4, (void**)&coff)) != hipSuccess) return fail(e);
+    if ((e = launch_chess_replay(d_text, d_fen_off, d_mv_off, ply_off, ngames, nullptr, states, d_final, err, s)) !=
+        hipSuccess)
+      return fail(e);
     uint32_t herr[4];
     if ((e = hipMemcpyAsync(herr, err, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
@@ -592,9 +656,10 @@ BuildResult build_batch_device(const char* d_text, const uint32_t* d_fen_off, co
     hipLaunchKernelGGL(count_children_kernel, dim3((total_plies + bs - 1) / bs), dim3(bs), 0, s, states,
                        total_plies, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
-    if ((e = builder_exclusive_scan(cnt, coff, total_plies, s)) != hipSuccess) return fail(e);
+    if ((e = builder_exclusive_scan(cnt, coff, total_plies, s, ws)) != hipSuccess) return fail(e);
     uint32_t total = 0;
-    if ((e = hipMemcpy(&total, coff + total_plies, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(&total, coff + total_plies, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
     R.n_out = total;
     R.n_groups = total_plies;
     if (cap < total || off_cap < (size_t)total_plies + 1 || !d_out || !d_group_off) {

@@ -65,6 +65,7 @@ void ctx_destroy(fnnue_ctx* c) {
   for (hipEvent_t e : {c->ws_event, c->dual_fork, c->dual_join})
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  c->bscratch.release();
   for (void* p : {(void*)c->image, (void*)c->x, (void*)c->bucket, (void*)c->err, (void*)c->d_pos, (void*)c->d_off, (void*)c->d_btext,
                   (void*)c->d_psqt, (void*)c->d_positional, c->plan.tiles, (void*)c->plan.ctr, c->plan.units,
                   (void*)c->plan.items, (void*)c->plan.flist, (void*)c->plan.perm,
@@ -1214,7 +1215,8 @@ int fnnue_build_batch_device(fnnue_ctx* ctx, const char* d_text, const uint32_t*
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const BuildResult R = build_batch_device(d_text, d_fen_off, d_moves_off, (uint32_t)ngames,
-                                           mode == FNNUE_PLAYOUT_CHILDREN, d_out, cap, d_off, off_cap, s);
+                                           mode == FNNUE_PLAYOUT_CHILDREN, d_out, cap, d_off, off_cap, s,
+                                           ctx->bscratch);
   if (R.hip != hipSuccess) return hip_fail(R.hip, "device batch builder");
   *n_out = R.n_out;
   *n_groups = R.n_groups;

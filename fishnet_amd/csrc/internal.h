@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/fnnue.h"
+#include "builder.h"
 #include "kernels.h"
 #include "net.h"
 
@@ -38,6 +39,7 @@ struct fnnue_ctx {
   size_t stage_cap = 0, off_cap = 0;
   char* d_btext = nullptr;     // fnnue_build_batch input staging (text, then FEN / move offsets), grow-only
   size_t btext_cap = 0;
+  fnnue::BuilderScratch bscratch;  // the device batch builder's temporaries, grow-only
   int ft_impl = FNNUE_FT_SLICED;
   int32_t acc_bound = 0;       // accumulator_bound of the net (SWAR rows allowed below 2^15)
   fnnue::SlicedPlan plan{};

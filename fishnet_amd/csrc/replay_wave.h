@@ -1,0 +1,244 @@
+// replay_wave.h — the batch builder's game replay, one 64-lane wave per game
+// (builder.hip: chess, vbuilder.hip: crazyhouse / atomic).
+//
+// IncomingBatch::from_acquired ([ref] src/queue.rs:543-606) parses a root FEN
+// and plays every UCI move of the batch, checking each (shakmaty's
+// Uci::to_move); the positions after every move are the batch.  Replay is a
+// chain (ply k needs ply k - 1), but only a small part of each ply is: what
+// the board becomes.  Whether the token names a legal move, and the packed
+// record, are per-ply work once the boards are known.  So a wave
+//   (a) tokenises the game's move text 64 characters at a time (lane =
+//       character: token starts by ballot, each starting lane decodes its
+//       token into a move code),
+//   (b) plays up to 64 moves in a row: interprets each code on the current
+//       board (castling / en passant / promotion / drop — no move generation)
+//       and applies it; every lane runs this wave-uniform chain, lane 0 keeps
+//       each board in LDS,
+//   (c) checks in parallel, lane j for move j, that the token names exactly
+//       the move (b) applied — the rules' match over the legal moves of the
+//       board before it (the same test the one-thread-per-ply host replay
+//       makes) — and packs the board after it into the output record,
+// and repeats until the game's text is consumed.  The first move whose check
+// fails ends the game with a latched error (the batch fails: PositionFailed);
+// boards after it are never written.  The last board gets the game-end flags
+// (no legal move / check / exploded king), its legal-move search split over
+// the lanes by from-square.
+//
+// Output offsets are the host's (ply_off: 1 + moves per game, counted with the
+// same whitespace rule), so no sizing pass or read-back is needed; a game
+// whose token count differs latches kBuildErrCount and writes nothing outside
+// its own range.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "builder.h"
+
+namespace fnnue {
+namespace replay {
+
+// Token codes: bits 0-5 from, 6-11 to, 12-14 promotion / drop piece type,
+// bit 15 drop, bit 31 malformed (no legal move can match it).
+constexpr uint32_t kTokBad = 1u << 31, kTokDrop = 1u << 15;
+__device__ __forceinline__ uint32_t tok_from(uint32_t c) { return c & 63; }
+__device__ __forceinline__ uint32_t tok_to(uint32_t c) { return (c >> 6) & 63; }
+__device__ __forceinline__ uint32_t tok_piece(uint32_t c) { return (c >> 12) & 7; }
+
+__device__ __forceinline__ int tok_sq(char f, char r) {
+  return (f >= 'a' && f <= 'h' && r >= '1' && r <= '8') ? (r - '1') * 8 + (f - 'a') : -1;
+}
+
+__device__ __forceinline__ bool space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+
+__device__ __forceinline__ void lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t game, uint32_t ply) {
+  if (atomicCAS(&err[0], 0u, code) == 0u) {
+    err[1] = game;
+    err[2] = ply;
+  }
+}
+
+constexpr int kFenLds = 256;   // FENs up to this length are parsed from LDS
+constexpr int kTokRing = 128;  // pending move codes (<= 63 left + 32 new per 64 characters)
+
+// Rules (builder.hip ChessRules, vbuilder.hip VariantRules):
+//   Board, Move, Pos
+//   bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant, Board&)
+//   uint32_t encode(const char* c, int len)             token -> code (kTokBad if malformed)
+//   bool interpret(const Board&, uint32_t code, Move&)   cheap: the move the code would be
+//   void do_move(Board&, const Move&)
+//   bool verify(const Board&, uint32_t code, const Move&) the code matches exactly this legal move
+//   Pos pack(const Board&)
+//   bool any_legal_from(const Board&, int sq, bool drops) legal moves of the piece on sq (+ drops)
+//   uint8_t end_flags(const Board&, bool any)             kFinal* of a last position
+template <class R>
+__global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char* __restrict__ text,
+                                                         const uint32_t* __restrict__ fen_off,
+                                                         const uint32_t* __restrict__ mv_off, uint32_t ngames,
+                                                         const uint32_t* __restrict__ ply_off,
+                                                         typename R::Pos* __restrict__ out,
+                                                         typename R::Board* __restrict__ states,
+                                                         uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
+  using Board = typename R::Board;
+  using Move = typename R::Move;
+  __shared__ Board S[65];           // S[0]: board before the window, S[j + 1]: after its move j
+  __shared__ Move MV[64];           // the moves (b) applied
+  __shared__ uint32_t TK[kTokRing]; // pending token codes
+  __shared__ char FEN[kFenLds];
+  const uint32_t g = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (g >= ngames) return;
+  const uint32_t f0 = fen_off[g], m0 = mv_off[g], e = fen_off[g + 1];
+  const uint32_t o0 = ply_off[g], nply = ply_off[g + 1] - o0;
+  if (nply == 0) {
+    if (lane == 0) latch(err, kBuildErrCount, g, 0);
+    return;
+  }
+  const uint32_t nmoves = nply - 1;
+
+  // ---- root: FEN through LDS, parsed by every lane alike ----
+  Board b;
+  bool ok;
+  const uint32_t flen = m0 - f0;
+  if (flen <= (uint32_t)kFenLds) {
+    for (uint32_t i = lane; i < flen; i += 64) FEN[i] = text[f0 + i];
+    lds_fence();
+    ok = R::parse_fen(FEN, 0, flen, variant, b);
+  } else {
+    ok = R::parse_fen(text, f0, m0, variant, b);
+  }
+  if (!ok) {
+    if (lane == 0) latch(err, kBuildErrFen, g, 0);
+    return;
+  }
+  if (lane == 0) {
+    if (out) out[o0] = R::pack(b);
+    if (states) states[o0] = b;
+  }
+
+  // ---- windows of up to 64 moves ----
+  uint32_t p = m0;   // next text character to tokenise
+  char prev = ' ';   // the character before p
+  uint32_t ntok = 0; // pending codes in TK[0 .. ntok)
+  uint32_t done = 0; // moves played and checked
+  uint32_t bad = 0;  // kBuildErr* of this game
+  uint32_t bad_ply = 0;
+  while (done < nmoves) {
+    // (a) tokenise until a full window is pending or the text ends
+    while (ntok < 64 && p < e) {
+      const uint32_t i = p + lane;
+      const char c = i < e ? text[i] : ' ';
+      const char cprev = (char)__shfl_up((int)c, 1, 64);
+      const bool start = !space(c) && space(lane == 0 ? prev : cprev);
+      const uint64_t starts = __ballot(start);
+      if (start) {
+        char t[6];
+        t[0] = c;
+        int len = 1;
+        bool more = true;
+#pragma unroll
+        for (int k = 1; k < 6; ++k) {
+          const char ck = (more && i + k < e) ? text[i + k] : ' ';
+          more = more && !space(ck);
+          t[k] = ck;
+          len += more ? 1 : 0;
+        }
+        const uint32_t code = (len == 4 || len == 5) ? R::encode(t, len) : kTokBad;
+        const uint32_t idx = ntok + (uint32_t)__popcll(starts & ((1ull << lane) - 1));
+        if (idx < (uint32_t)kTokRing) TK[idx] = code;
+      }
+      ntok += (uint32_t)__popcll(starts);
+      prev = (char)__shfl((int)c, 63, 64);
+      p += 64;
+    }
+    lds_fence();
+    if (ntok == 0 || ntok > (uint32_t)kTokRing) {  // fewer tokens than the host counted (or a ring overrun)
+      bad = kBuildErrCount;
+      bad_ply = done + 1;
+      break;
+    }
+    const uint32_t k = min(min(ntok, 64u), nmoves - done);
+    // (b) the chain: interpret and play each move, boards to LDS
+    if (lane == 0) S[0] = b;
+    uint32_t kplay = k;
+    for (uint32_t j = 0; j < k; ++j) {
+      const uint32_t code = TK[j];
+      Move m;
+      if ((code & kTokBad) || !R::interpret(b, code, m)) {
+        kplay = j;
+        break;
+      }
+      R::do_move(b, m);
+      if (lane == 0) {
+        S[j + 1] = b;
+        MV[j] = m;
+      }
+    }
+    lds_fence();
+    // (c) lane j checks move j against the board before it and packs the board after it
+    bool fail = false;
+    if ((uint32_t)lane < kplay) {
+      const Board before = S[lane];
+      fail = !R::verify(before, TK[lane], MV[lane]);
+      if (!fail) {
+        const Board after = S[lane + 1];
+        const uint32_t o = o0 + done + lane + 1;
+        if (out) out[o] = R::pack(after);
+        if (states) states[o] = after;
+      }
+    }
+    const uint64_t fails = __ballot(fail);
+    const uint32_t first = fails ? (uint32_t)__builtin_ctzll(fails) : kplay;
+    if (first < k) {
+      bad = kBuildErrMove;
+      bad_ply = done + first + 1;
+      break;
+    }
+    done += k;
+    ntok -= k;
+    // drop the consumed codes
+    uint32_t keep[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t src = k + lane + 64 * r;
+      keep[r] = src < (uint32_t)kTokRing ? TK[src] : 0;
+    }
+    lds_fence();
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      if ((uint32_t)lane + 64 * r < ntok) TK[lane + 64 * r] = keep[r];
+    lds_fence();
+  }
+  if (!bad) {
+    // text left after the host's count: more tokens than plies
+    bool extra = ntok != 0;
+    for (uint32_t q = p; q < e && !extra; q += 64) {
+      const uint32_t i = q + lane;
+      const char c = i < e ? text[i] : ' ';
+      const char cprev = (char)__shfl_up((int)c, 1, 64);
+      extra = __ballot(!space(c) && space(lane == 0 ? prev : cprev)) != 0;
+      prev = (char)__shfl((int)c, 63, 64);
+    }
+    if (extra) {
+      bad = kBuildErrCount;
+      bad_ply = nmoves + 1;
+    }
+  }
+  if (bad) {
+    if (lane == 0) latch(err, bad, g, bad_ply);
+    return;
+  }
+  if (final) {
+    const bool any = __ballot(R::any_legal_from(b, lane, lane == 0)) != 0;
+    if (lane == 0) final[g] = R::end_flags(b, any);
+  }
+}
+
+}  // namespace replay
+}  // namespace fnnue

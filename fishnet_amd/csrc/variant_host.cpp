@@ -403,7 +403,8 @@ int fnnue_build_vbatch_device(fnnue_ctx* ctx, int variant, const char* d_text, c
   DeviceGuard g(ctx->device);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
   const BuildResult R = build_vbatch_device(variant, d_text, d_fen_off, d_moves_off, (uint32_t)ngames,
-                                            mode == FNNUE_PLAYOUT_CHILDREN, d_out, cap, d_off, off_cap, s);
+                                            mode == FNNUE_PLAYOUT_CHILDREN, d_out, cap, d_off, off_cap, s,
+                                            ctx->bscratch);
   if (R.hip != hipSuccess) return hip_fail(R.hip, "device variant batch builder");
   *n_out = R.n_out;
   *n_groups = R.n_groups;

@@ -473,6 +473,34 @@ FNNUE_HD bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant,
   return true;
 }
 
+// The legal move a decoded token names: a drop of `piece` on `to` (drop), or
+// the move from `from` to `to` with promotion `piece` (0 none), castling as
+// king-takes-rook or (standard positions) the king's two-square step.
+FNNUE_HD bool match_decoded(const VBoard& b, int from, int to, int piece, bool drop, VMove& out) {
+  bool found = false;
+  if (drop) {
+    for_each_legal(b, [&](const VMove& m) -> bool {
+      if (m.piece == piece && m.to == to) {
+        out = m;
+        found = true;
+        return false;
+      }
+      return true;
+    }, 0ull, false, true);
+    return found;
+  }
+  for_each_legal(b, [&](const VMove& m) -> bool {
+    if (m.from != from || (m.kind != 1 && m.piece != piece) || (m.kind == 1 && piece)) return true;
+    const bool hit = m.to == to || (m.kind == 1 && !b.c960 && to == (m.from & 56) + (m.to > m.from ? 6 : 2));
+    if (hit) {
+      out = m;
+      found = true;
+    }
+    return !hit;
+  }, 1ull << from, true, false);
+  return found;
+}
+
 // The legal move whose UCI text equals the token: "e2e4", "e7e8q", castling as
 // king-takes-rook or (standard positions) the king's two-square step, drops
 // as "P@e4" (either case).
@@ -481,19 +509,10 @@ FNNUE_HD bool match_uci(const VBoard& b, const char* tok, int len, VMove& out) {
     const char f = tok[i], r = tok[i + 1];
     return (f >= 'a' && f <= 'h' && r >= '1' && r <= '8') ? (r - '1') * 8 + (f - 'a') : -1;
   };
-  bool found = false;
   if (len == 4 && tok[1] == '@') {
     const int pt = piece_type_of(tok[0]), to = sqr(2);
     if (!pt || pt == KING || to < 0) return false;
-    for_each_legal(b, [&](const VMove& m) -> bool {
-      if (m.piece == pt && m.to == to) {
-        out = m;
-        found = true;
-        return false;
-      }
-      return true;
-    }, 0ull, false, true);
-    return found;
+    return match_decoded(b, -1, to, pt, true, out);
   }
   if (len != 4 && len != 5) return false;
   const int from = sqr(0), to = sqr(2);
@@ -503,16 +522,7 @@ FNNUE_HD bool match_uci(const VBoard& b, const char* tok, int len, VMove& out) {
     promo = piece_type_of(tok[4]);
     if (!promo || promo == PAWN || promo == KING) return false;
   }
-  for_each_legal(b, [&](const VMove& m) -> bool {
-    if (m.from != from || (m.kind != 1 && m.piece != promo) || (m.kind == 1 && promo)) return true;
-    const bool hit = m.to == to || (m.kind == 1 && !b.c960 && to == (m.from & 56) + (m.to > m.from ? 6 : 2));
-    if (hit) {
-      out = m;
-      found = true;
-    }
-    return !hit;
-  }, 1ull << from, true, false);
-  return found;
+  return match_decoded(b, from, to, promo, false, out);
 }
 
 #undef FNNUE_HD

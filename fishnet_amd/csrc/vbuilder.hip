@@ -3,9 +3,9 @@
 // ([ref] src/queue.rs:524-552 with body.variant != Standard, routed to the
 // MultiVariant engine at :530-539; variants from src/assets.rs:384-391).
 //
-// As builder.hip for chess: one thread per game parses the FEN (holdings,
-// promoted marks) and replays the UCI moves (drops "P@e4", pockets,
-// explosions) with the rules of vboard.h — the same source the host replay
+// As builder.hip for chess: one wave per game (replay_wave.h) parses the FEN
+// (holdings, promoted marks) and replays the UCI moves (drops "P@e4",
+// pockets, explosions) with the rules of vboard.h — the same source the host replay
 // (fnnue_game_vpositions) runs, which the tests hold it to record for record —
 // writing one fnnue_vpos per ply; CHILDREN adds one thread per ply for its
 // legal children (drops included).
@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "builder.h"
+#include "replay_wave.h"
 #include "vboard.h"
 
 namespace fnnue {
@@ -31,45 +32,79 @@ __global__ void vcount_plies_kernel(const char* __restrict__ text, const uint32_
   plies[g] = n;
 }
 
-__device__ __forceinline__ void vlatch(uint32_t* err, uint32_t code, uint32_t game, uint32_t ply) {
-  if (atomicCAS(&err[0], 0u, code) == 0u) {
-    err[1] = game;
-    err[2] = ply;
+// Variant rules of the wave replay (replay_wave.h), vboard.h's.
+struct VariantRules {
+  using Board = vb::VBoard;
+  using Move = vb::VMove;
+  using Pos = fnnue_vpos;
+  __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int variant, vb::VBoard& b) {
+    return vb::parse_fen(t, p, e, variant, b);
   }
-}
-
-__global__ void vreplay_kernel(int variant, const char* __restrict__ text, const uint32_t* __restrict__ fen_off,
-                               const uint32_t* __restrict__ mv_off, uint32_t ngames,
-                               const uint32_t* __restrict__ ply_off, fnnue_vpos* __restrict__ out,
-                               vb::VBoard* __restrict__ states, uint32_t* __restrict__ err,
-                               uint8_t* __restrict__ final) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= ngames) return;
-  vb::VBoard b;
-  if (!vb::parse_fen(text, fen_off[g], mv_off[g], variant, b)) {
-    vlatch(err, kBuildErrFen, g, 0);
-    return;
-  }
-  uint32_t o = ply_off[g];
-  if (out) out[o] = vb::pack(b);
-  if (states) states[o] = b;
-  uint32_t p = mv_off[g], st, ply = 0;
-  const uint32_t end = fen_off[g + 1];
-  int len;
-  while ((len = vb::next_token(text, p, end, st)) > 0) {
-    ++ply;
-    vb::VMove m;
-    if (!vb::match_uci(b, text + st, len, m)) {
-      vlatch(err, kBuildErrMove, g, ply);
-      return;
+  // vb::match_uci's token rules: drops "P@e4" (piece letter either case, no
+  // king), moves "e2e4" / "e7e8q" (promotion letter either case, N B R Q)
+  __device__ static uint32_t encode(const char* c, int len) {
+    if (len == 4 && c[1] == '@') {
+      const int pt = vb::piece_type_of(c[0]), to = replay::tok_sq(c[2], c[3]);
+      if (!pt || pt == vb::KING || to < 0) return replay::kTokBad;
+      return ((uint32_t)to << 6) | ((uint32_t)pt << 12) | replay::kTokDrop;
     }
-    vb::do_move(b, m);
-    ++o;
-    if (out) out[o] = vb::pack(b);
-    if (states) states[o] = b;
+    const int from = replay::tok_sq(c[0], c[1]), to = replay::tok_sq(c[2], c[3]);
+    if (from < 0 || to < 0) return replay::kTokBad;
+    int promo = 0;
+    if (len == 5) {
+      promo = vb::piece_type_of(c[4]);
+      if (!promo || promo == vb::PAWN || promo == vb::KING) return replay::kTokBad;
+    }
+    return (uint32_t)from | ((uint32_t)to << 6) | ((uint32_t)promo << 12);
   }
-  if (final) final[g] = vb::final_state(b);
-}
+  __device__ static bool interpret(const vb::VBoard& b, uint32_t code, vb::VMove& m) {
+    const int to = (int)replay::tok_to(code), pc = (int)replay::tok_piece(code);
+    if (code & replay::kTokDrop) {
+      m = vb::VMove{-1, (int8_t)to, (int8_t)pc, 2};
+      return true;
+    }
+    const int from = (int)replay::tok_from(code);
+    const uint64_t fm = 1ull << from;
+    if (!(b.bc[b.stm] & fm)) return false;
+    m = vb::VMove{(int8_t)from, (int8_t)to, (int8_t)pc, 0};
+    if ((b.bt[vb::KING] & fm) && !pc) {
+      const int back = b.stm == 0 ? 0 : 56;
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {
+        const int rsq = b.cr[b.stm][side];
+        if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
+          m = vb::VMove{(int8_t)from, (int8_t)rsq, 0, 1};
+          return true;
+        }
+      }
+    }
+    return true;
+  }
+  __device__ static void do_move(vb::VBoard& b, const vb::VMove& m) { vb::do_move(b, m); }
+  __device__ static bool verify(const vb::VBoard& b, uint32_t code, const vb::VMove& m) {
+    vb::VMove x;
+    const bool drop = code & replay::kTokDrop;
+    const bool ok = vb::match_decoded(b, drop ? -1 : (int)replay::tok_from(code), (int)replay::tok_to(code),
+                                      (int)replay::tok_piece(code), drop, x);
+    return ok && x.from == m.from && x.to == m.to && x.piece == m.piece && x.kind == m.kind;
+  }
+  __device__ static fnnue_vpos pack(const vb::VBoard& b) { return vb::pack(b); }
+  __device__ static bool any_legal_from(const vb::VBoard& b, int sq, bool drops) {
+    const bool own = (b.bc[b.stm] >> sq) & 1;
+    if (!own && !drops) return false;
+    bool any = false;
+    vb::for_each_legal(b, [&](const vb::VMove&) -> bool {
+      any = true;
+      return false;
+    }, own ? 1ull << sq : 0ull, own, drops);
+    return any;
+  }
+  __device__ static uint8_t end_flags(const vb::VBoard& b, bool any) {
+    const int us = b.stm, k = vb::king_sq(b, us);
+    const bool check = k >= 0 && vb::king_danger(b, k, us, vb::occupied(b));
+    return (uint8_t)((any ? 0 : kFinalNoMoves) | (check ? kFinalCheck : 0) | (k < 0 ? kFinalExtinct : 0));
+  }
+};
 
 __global__ void vcount_children_kernel(const vb::VBoard* __restrict__ states, uint32_t n, uint32_t* __restrict__ cnt) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -100,9 +135,19 @@ __global__ void vwrite_children_kernel(const vb::VBoard* __restrict__ states, ui
 
 }  // namespace
 
+hipError_t replay_vgames_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                                const uint32_t* d_ply_off, uint32_t ngames, fnnue_vpos* d_out, void* d_states,
+                                uint8_t* d_final, uint32_t* d_err, hipStream_t s) {
+  if (!ngames) return hipSuccess;
+  hipLaunchKernelGGL(replay::replay_wave_kernel<VariantRules>, dim3(ngames), dim3(64), 0, s, variant, d_text,
+                     d_fen_off, d_mv_off, ngames, d_ply_off, d_out, static_cast<vb::VBoard*>(d_states), d_err,
+                     d_final);
+  return hipGetLastError();
+}
+
 BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                 uint32_t ngames, bool children, fnnue_vpos* d_out, size_t cap, uint32_t* d_group_off,
-                                size_t off_cap, hipStream_t s, uint8_t* d_final) {
+                                size_t off_cap, hipStream_t s, BuilderScratch& ws, uint8_t* d_final) {
   BuildResult R;
   auto fail = [&](hipError_t e) {
     R.hip = e;
@@ -111,29 +156,20 @@ BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t*
   hipError_t e;
   uint32_t *plies = nullptr, *ply_off = nullptr, *err = nullptr, *cnt = nullptr, *coff = nullptr;
   vb::VBoard* states = nullptr;
-  struct Free {
-    std::vector<void*> p;
-    ~Free() {
-      for (void* x : p) (void)hipFree(x);
-    }
-  } F;
-  auto alloc = [&](void** p, size_t bytes) {
-    hipError_t a = hipMalloc(p, bytes ? bytes : 4);
-    if (a == hipSuccess) F.p.push_back(*p);
-    return a;
-  };
-  if ((e = alloc((void**)&plies, (size_t)(ngames + 1) * 4)) != hipSuccess) return fail(e);
-  if ((e = alloc((void**)&ply_off, (size_t)(ngames + 1) * 4)) != hipSuccess) return fail(e);
-  if ((e = alloc((void**)&err, 16)) != hipSuccess) return fail(e);
+  using W = BuilderScratch;
+  if ((e = ws.get(W::kPlies, (size_t)(ngames + 1) * 4, (void**)&plies)) != hipSuccess) return fail(e);
+  if ((e = ws.get(W::kPlyOff, (size_t)(ngames + 1) * 4, (void**)&ply_off)) != hipSuccess) return fail(e);
+  if ((e = ws.get(W::kErr, 16, (void**)&err)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(err, 0, 16, s)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(plies + ngames, 0, 4, s)) != hipSuccess) return fail(e);
   const uint32_t bs = 64;
   hipLaunchKernelGGL(vcount_plies_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, d_text, d_fen_off, d_mv_off,
                      ngames, plies);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e);
-  if ((e = builder_exclusive_scan(plies, ply_off, ngames, s)) != hipSuccess) return fail(e);
+  if ((e = builder_exclusive_scan(plies, ply_off, ngames, s, ws)) != hipSuccess) return fail(e);
   uint32_t total_plies = 0;
-  if ((e = hipMemcpy(&total_plies, ply_off + ngames, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
+  if ((e = hipMemcpyAsync(&total_plies, ply_off + ngames, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
   if (!children) {
     R.n_out = total_plies;
     R.n_groups = ngames;
@@ -141,19 +177,20 @@ BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t*
       R.capacity = true;
       return R;
     }
-    hipLaunchKernelGGL(vreplay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, variant, d_text, d_fen_off,
-                       d_mv_off, ngames, ply_off, d_out, (vb::VBoard*)nullptr, err, d_final);
-    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = replay_vgames_device(variant, d_text, d_fen_off, d_mv_off, ply_off, ngames, d_out, nullptr, d_final, err,
+                                  s)) != hipSuccess)
+      return fail(e);
     if ((e = hipMemcpyAsync(d_group_off, ply_off, (size_t)(ngames + 1) * 4, hipMemcpyDeviceToDevice, s)) !=
         hipSuccess)
       return fail(e);
   } else {
-    if ((e = alloc((void**)&states, (size_t)total_plies * sizeof(vb::VBoard))) != hipSuccess) return fail(e);
-    if ((e = alloc((void**)&cnt, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
-    if ((e = alloc((void**)&coff, (size_t)(total_plies + 1) * 4)) != hipSuccess) return fail(e);
-    hipLaunchKernelGGL(vreplay_kernel, dim3((ngames + bs - 1) / bs), dim3(bs), 0, s, variant, d_text, d_fen_off,
-                       d_mv_off, ngames, ply_off, (fnnue_vpos*)nullptr, states, err, d_final);
-    if ((e = hipGetLastError()) != hipSuccess) return fail(e);
+    if ((e = ws.get(W::kStates, (size_t)total_plies * sizeof(vb::VBoard), (void**)&states)) != hipSuccess)
+      return fail(e);
+    if ((e = ws.get(W::kCnt, (size_t)(total_plies + 1) * 4, (void**)&cnt)) != hipSuccess) return fail(e);
+    if ((e = ws.get(W::kCoff, (size_t)(total_plies + 1) * 4, (void**)&coff)) != hipSuccess) return fail(e);
+    if ((e = replay_vgames_device(variant, d_text, d_fen_off, d_mv_off, ply_off, ngames, nullptr, states, d_final,
+                                  err, s)) != hipSuccess)
+      return fail(e);
     uint32_t herr[4];
     if ((e = hipMemcpyAsync(herr, err, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
@@ -167,9 +204,10 @@ BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t*
     hipLaunchKernelGGL(vcount_children_kernel, dim3((total_plies + bs - 1) / bs), dim3(bs), 0, s, states,
                        total_plies, cnt);
     if ((e = hipGetLastError()) != hipSuccess) return fail(e);
-    if ((e = builder_exclusive_scan(cnt, coff, total_plies, s)) != hipSuccess) return fail(e);
+    if ((e = builder_exclusive_scan(cnt, coff, total_plies, s, ws)) != hipSuccess) return fail(e);
     uint32_t total = 0;
-    if ((e = hipMemcpy(&total, coff + total_plies, 4, hipMemcpyDeviceToHost)) != hipSuccess) return fail(e);
+    if ((e = hipMemcpyAsync(&total, coff + total_plies, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return fail(e);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return fail(e);
     R.n_out = total;
     R.n_groups = total_plies;
     if (cap < total || off_cap < (size_t)total_plies + 1 || !d_out || !d_group_off) {

@@ -135,6 +135,24 @@ int fnnue_backend_batch_size(const fnnue_acquired *a, size_t *n);
 int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nbatches, fnnue_position_response *out,
                      size_t cap, uint32_t *off, int32_t *batch_rc);
 
+/* Where the last go() spent its time (diagnostics; the reference's engine
+ * reports only time / nps per position).  One net's work is one host-to-
+ * device copy, the replay and evaluation kernels, one device-to-host copy of
+ * the results and of the evaluator's error word, and one wait. */
+typedef struct {
+  double prep_ms;         /* host: sizes, move-work roots, text staging, copies and kernels enqueued */
+  double device_ms;       /* from then until every net's results are on the host */
+  double fill_ms;         /* responses written */
+  double total_ms;
+  uint64_t positions;     /* positions evaluated (analysis plies + move-work children) */
+  uint32_t stream_syncs;  /* host waits on a stream or a blocking copy */
+  uint32_t rebuilds;      /* extra passes after a batch failed (per failed batch, its net only) */
+  uint32_t host_threads;  /* threads for the staging / fill loops (FNNUE_BACKEND_THREADS, default <= 8) */
+  uint32_t reserved;
+} fnnue_backend_stats;
+
+int fnnue_backend_last_stats(fnnue_backend *b, fnnue_backend_stats *out);
+
 /* The `analysis` array fishnet submits for one analysis batch
  * (CompletedBatch::into_analysis, queue.rs:715-727; AnalysisPart / Score
  * serialisation, api.rs:355-388): {"skipped":true} or {"score":{"cp":..},

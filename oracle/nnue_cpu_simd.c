@@ -365,6 +365,94 @@ int cpu_simd_eval_groups(const onet *n, const uint8_t *packed, const uint32_t *o
     return s_run(n, packed, off, mode, ngroups, psqt, positional, threads);
 }
 
+/* ---- whole analysis batches: expansion + evaluation (bench.py --workload backend) ----
+ * What the reference's host does per acquired batch, restated: parse the root
+ * FEN, play the UCI moves one by one (IncomingBatch::from_acquired, [ref]
+ * src/queue.rs:571-606; here the oracle's own minimal board code, without the
+ * legality checks shakmaty makes, so the baseline is if anything flattered),
+ * then evaluate every ply with accumulators carried along the game (the
+ * engine's StateInfo chain).  Game g's FEN is text[fen_off[g] .. mv_off[g]),
+ * its moves text[mv_off[g] .. fen_off[g + 1]); its results go to
+ * ps/po[out_off[g] ..] (out_off[g + 1] - out_off[g] = plies).  Threads split
+ * the games. */
+typedef struct {
+    const onet *n;
+    const char *text;
+    const uint32_t *fen_off, *mv_off, *out_off;
+    size_t b, e;
+    int32_t *ps, *po;
+    int rc;
+} s_games_job;
+
+static void s_pack(const uint8_t *board, int stm, uint8_t *p36) {
+    for (int i = 0; i < 32; ++i) p36[i] = (uint8_t)(board[2 * i] | (board[2 * i + 1] << 4));
+    p36[32] = (uint8_t)stm;
+    p36[33] = p36[34] = p36[35] = 0;
+}
+
+static void *s_games_worker(void *arg) {
+    s_games_job *j = (s_games_job *)arg;
+    s_state *st = (s_state *)aligned_alloc(64, (2 * sizeof(s_state) + 63) & ~(size_t)63);
+    char *fen = (char *)malloc(256);
+    if (!st || !fen) { free(st); free(fen); j->rc = -2; return NULL; }
+    int bad = 0;
+    for (size_t g = j->b; g < j->e && !bad; ++g) {
+        const uint32_t f0 = j->fen_off[g], m0 = j->mv_off[g], end = j->fen_off[g + 1];
+        const uint32_t flen = m0 - f0 < 255 ? m0 - f0 : 255;
+        memcpy(fen, j->text + f0, flen);
+        fen[flen] = 0;
+        uint8_t board[64], p36[36];
+        int stm, ep;
+        if (oracle_board_from_fen(fen, board, &stm, &ep)) { bad = 1; break; }
+        const uint32_t o = j->out_off[g], nply = j->out_off[g + 1] - o;
+        uint32_t k = 0, p = m0;
+        for (;;) {
+            s_pack(board, stm, p36);
+            const s_state *base = k == 0 ? NULL : &st[(k - 1) & 1];
+            bad |= s_eval_from(j->n, p36, base, &st[k & 1], &j->ps[o + k], &j->po[o + k]) != 0;
+            if (++k >= nply) break;
+            while (p < end && j->text[p] == ' ') ++p;
+            char tok[8];
+            int len = 0;
+            while (p < end && j->text[p] != ' ') {
+                if (len < 7) tok[len++] = j->text[p];
+                ++p;
+            }
+            tok[len] = 0;
+            if (!len || oracle_apply_uci(board, &stm, &ep, tok)) { bad = 1; break; }
+        }
+    }
+    free(fen);
+    free(st);
+    j->rc = bad ? -1 : 0;
+    return NULL;
+}
+
+int cpu_simd_eval_games(const onet *n, const char *text, const uint32_t *fen_off, const uint32_t *mv_off,
+                        size_t ngames, const uint32_t *out_off, int32_t *psqt, int32_t *positional, int threads) {
+    if (n->hd > S_MAX_HD || n->hd % 64) return -3;
+    s_use512();
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    s_games_job jobs[256];
+    const size_t per = (ngames + threads - 1) / threads;
+    int started = 0;
+    for (int t = 0; t < threads; ++t) {
+        const size_t b = (size_t)t * per, e = b + per > ngames ? ngames : b + per;
+        if (b >= e) break;
+        jobs[t] = (s_games_job){ n, text, fen_off, mv_off, out_off, b, e, psqt, positional, 0 };
+        pthread_create(&tid[t], NULL, s_games_worker, &jobs[t]);
+        ++started;
+    }
+    int rc = 0;
+    for (int t = 0; t < started; ++t) {
+        pthread_join(tid[t], NULL);
+        if (jobs[t].rc) rc = rc ? rc : jobs[t].rc;
+    }
+    return rc;
+}
+
 /* 1 if the AVX-512 VNNI paths are in use on this host (FNNUE_CPU_ISA=avx2 forces AVX2). */
 int cpu_simd_isa512(void) { return s_use512(); }
 

@@ -44,6 +44,8 @@ typedef struct {
 
 int oracle_make_index(int persp, int s, int pc, int ksq);
 int oracle_eval_board(const onet *n, const uint8_t *board, int stm, int32_t *psqt_out, int32_t *pos_out);
+int oracle_board_from_fen(const char *fen, uint8_t *board, int *stm, int *ep);
+int oracle_apply_uci(uint8_t *board, int *stm, int *ep, const char *uci);
 
 /* Shared by the chess and the variant restatements: FeatureTransformer::
  * transform + Network[bucket]::propagate from the two perspectives'

@@ -44,6 +44,8 @@ def _load() -> C.CDLL:
     lib.cpu_simd_eval_packed.restype = C.c_int
     lib.cpu_simd_eval_groups.argtypes = [vp, vp, vp, C.c_size_t, C.c_int, vp, vp, C.c_int]
     lib.cpu_simd_eval_groups.restype = C.c_int
+    lib.cpu_simd_eval_games.argtypes = [vp, C.c_char_p, vp, vp, C.c_size_t, vp, vp, vp, C.c_int]
+    lib.cpu_simd_eval_games.restype = C.c_int
     lib.cpu_simd_isa512.restype = C.c_int
     lib.cpu_simd_set_isa.argtypes = [C.c_int]
     lib.cpu_simd_set_isa.restype = C.c_int
@@ -119,6 +121,21 @@ class OracleNet:
         rc = lib.cpu_simd_eval_groups(self._h, pos.ctypes.data, off.ctypes.data, len(off) - 1, mode,
                                       ps.ctypes.data, po.ctypes.data, threads)
         return ps, po, rc
+
+    def simd_eval_games(self, text: bytes, fen_off: np.ndarray, mv_off: np.ndarray, out_off: np.ndarray,
+                        threads: int = 1) -> tuple[np.ndarray, np.ndarray, int]:
+        """Whole analysis batches on the CPU: FEN parse + UCI replay + every ply
+        evaluated along the game (fishnet_amd.pack_games text layout; out_off =
+        per-game result offsets), AVX2 / AVX-512."""
+        fen_off = np.ascontiguousarray(fen_off, dtype=np.uint32)
+        mv_off = np.ascontiguousarray(mv_off, dtype=np.uint32)
+        out_off = np.ascontiguousarray(out_off, dtype=np.uint32)
+        n = int(out_off[-1])
+        ps = np.zeros(max(n, 1), dtype=np.int32)
+        po = np.zeros(max(n, 1), dtype=np.int32)
+        rc = lib.cpu_simd_eval_games(self._h, text, fen_off.ctypes.data, mv_off.ctypes.data, len(mv_off),
+                                     out_off.ctypes.data, ps.ctypes.data, po.ctypes.data, threads)
+        return ps[:n], po[:n], rc
 
     def eval_board(self, board: np.ndarray, stm: int) -> tuple[int, int]:
         board = np.ascontiguousarray(board, dtype=np.uint8)
