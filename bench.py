@@ -78,6 +78,7 @@ def parse_args():
                     help="backend workload: acquired batches per fnnue_backend_go call (comma list; the value is the "
                          "largest)")
     ap.add_argument("--go-seconds", type=float, default=1.5, help="backend workload: timed wall per batch count")
+    ap.add_argument("--go-calls", type=int, default=0, help="backend workload: exactly this many timed calls per count")
     ap.add_argument("--positions", type=int, default=1_000_000, help="positions per GPU (positions / variant workloads)")
     ap.add_argument("--games", type=int, default=None,
                     help="games per GPU (games: 10,000 = config 3; children: 5,000 ~ 12.5M positions per GPU = "
@@ -330,18 +331,25 @@ def main_backend(args):
         go(k)
         probe = time.perf_counter() - tp
         reps = int(min(2000, max(args.steps if args.steps < 1000 else 3, args.go_seconds / max(probe, 1e-6))))
-        times = []
+        if args.go_calls:
+            reps = args.go_calls
+        times, phases = [], []
         for _ in range(reps):
             tp = time.perf_counter()
             go(k)
             times.append(time.perf_counter() - tp)
+            phases.append(B.last_stats(actor))
         t = np.array(times)
+        ph = {key: round(float(np.mean([p[key] for p in phases])), 4)
+              for key in ("prep_ms", "device_ms", "fill_ms", "total_ms")}
+        ph["stream_syncs_per_go"] = float(np.mean([p["stream_syncs"] for p in phases]))
+        ph["host_threads"] = phases[-1]["host_threads"]
         assert not rc[:k].any(), "a synthetic batch failed"
         rows.append({"batches_per_go": k, "positions_per_go": npk, "calls": reps,
                      "ms_per_go_mean": round(float(t.mean()) * 1e3, 4),
                      "ms_per_go_median": round(float(np.median(t)) * 1e3, 4),
                      "ms_per_go_min": round(float(t.min()) * 1e3, 4),
-                     "positions_per_s": npk / float(t.mean())})
+                     "positions_per_s": npk / float(t.mean()), "actor_phases_ms": ph})
     top = rows[-1]
     kmax = top["batches_per_go"]
     # results of the last (largest) call: parity spot check + CPU baseline on the chess batches

@@ -33,6 +33,12 @@ namespace {
 constexpr uint64_t kNotA = 0xFEFEFEFEFEFEFEFEull, kNotH = 0x7F7F7F7F7F7F7F7Full;
 constexpr uint64_t kNotAB = 0xFCFCFCFCFCFCFCFCull, kNotGH = 0x3F3F3F3F3F3F3F3Full;
 
+// Every rule below is force-inlined and indexes the board's arrays only with
+// compile-time indices (colour and castling-rook accessors select instead of
+// indexing): a board passed by reference to an out-of-line function, or an
+// array indexed at run time, lives in scratch memory, and the replay's board
+// chain then waits on scratch loads every ply.
+
 __device__ __forceinline__ int lsb(uint64_t b) { return __builtin_ctzll(b); }
 
 __device__ __forceinline__ uint64_t knight_att(int s) {
@@ -53,43 +59,71 @@ __device__ __forceinline__ uint64_t pawn_att(int c, int s) {
   return c == WHITE ? ((b << 9) & kNotA) | ((b << 7) & kNotH) : ((b >> 7) & kNotA) | ((b >> 9) & kNotH);
 }
 
-__device__ __forceinline__ uint64_t ray(int s, int dr, int df, uint64_t occ) {
-  uint64_t a = 0;
-  int r = (s >> 3) + dr, f = (s & 7) + df;
-  while (r >= 0 && r < 8 && f >= 0 && f < 8) {
-    const int t = r * 8 + f;
-    a |= 1ull << t;
-    if (occ & (1ull << t)) break;
-    r += dr;
-    f += df;
-  }
-  return a;
+// Sliding attacks by occluded fill (Kogge-Stone): a fixed instruction
+// sequence, so lanes holding different boards never diverge.  SH > 0 shifts
+// left; `mask` removes squares that wrapped around a board edge.
+template <int SH>
+__device__ __forceinline__ uint64_t shl(uint64_t b) {
+  return SH > 0 ? b << SH : b >> -SH;
+}
+template <int SH>
+__device__ __forceinline__ uint64_t fill(uint64_t gen, uint64_t empty, uint64_t mask) {
+  uint64_t pro = empty & mask;
+  gen |= pro & shl<SH>(gen);
+  pro &= shl<SH>(pro);
+  gen |= pro & shl<2 * SH>(gen);
+  pro &= shl<2 * SH>(pro);
+  gen |= pro & shl<4 * SH>(gen);
+  return shl<SH>(gen) & mask;
 }
 
 __device__ __forceinline__ uint64_t bishop_att(int s, uint64_t occ) {
-  return ray(s, 1, 1, occ) | ray(s, 1, -1, occ) | ray(s, -1, 1, occ) | ray(s, -1, -1, occ);
+  const uint64_t g = 1ull << s, e = ~occ;
+  return fill<9>(g, e, kNotA) | fill<7>(g, e, kNotH) | fill<-7>(g, e, kNotA) | fill<-9>(g, e, kNotH);
 }
 __device__ __forceinline__ uint64_t rook_att(int s, uint64_t occ) {
-  return ray(s, 1, 0, occ) | ray(s, -1, 0, occ) | ray(s, 0, 1, occ) | ray(s, 0, -1, occ);
+  const uint64_t g = 1ull << s, e = ~occ;
+  return fill<8>(g, e, ~0ull) | fill<-8>(g, e, ~0ull) | fill<1>(g, e, kNotA) | fill<-1>(g, e, kNotH);
 }
 
 struct DMove {
   int from, to, promo, castle;  // castle: to = rook square (king takes rook)
 };
 
+__device__ __forceinline__ uint64_t colour(const DBoard& b, int c) { return c ? b.bc[1] : b.bc[0]; }
+
+__device__ __forceinline__ int cr_get(const DBoard& b, int c, int side) {
+  return c ? (side ? b.cr[1][1] : b.cr[1][0]) : (side ? b.cr[0][1] : b.cr[0][0]);
+}
+__device__ __forceinline__ void cr_clear(DBoard& b, int c) {
+  if (c) {
+    b.cr[1][0] = b.cr[1][1] = -1;
+  } else {
+    b.cr[0][0] = b.cr[0][1] = -1;
+  }
+}
+
+// Piece type on the square(s) of mask m (0: empty).
+__device__ __forceinline__ int type_at(const DBoard& b, uint64_t m) {
+  int t = 0;
+#pragma unroll
+  for (int k = 1; k <= KING; ++k) t = (b.bt[k] & m) ? k : t;
+  return t;
+}
+
 __device__ __forceinline__ int piece_at(const DBoard& b, int s) {
   const uint64_t m = 1ull << s;
-  if (!((b.bc[0] | b.bc[1]) & m)) return 0;
-  const int c = (b.bc[1] & m) ? 1 : 0;
-  int t = 1;
-  while (t < KING && !(b.bt[t] & m)) ++t;
-  return make_piece_d(c, t);
+  const int t = type_at(b, m);
+  return t ? make_piece_d((b.bc[1] & m) ? 1 : 0, t) : 0;
 }
 
 __device__ __forceinline__ void put(DBoard& b, int s, int pc) {
   const uint64_t m = 1ull << s;
-  b.bc[pc >> 3] |= m;
-  b.bt[pc & 7] |= m;
+  const int c = pc >> 3, t = pc & 7;
+  b.bc[0] |= c ? 0ull : m;
+  b.bc[1] |= c ? m : 0ull;
+#pragma unroll
+  for (int k = 1; k <= KING; ++k) b.bt[k] |= k == t ? m : 0ull;
 }
 
 __device__ __forceinline__ void remove_sq(DBoard& b, int s) {
@@ -101,22 +135,19 @@ __device__ __forceinline__ void remove_sq(DBoard& b, int s) {
 }
 
 __device__ __forceinline__ int king_sq(const DBoard& b, int c) {
-  const uint64_t k = b.bt[KING] & b.bc[c];
+  const uint64_t k = b.bt[KING] & colour(b, c);
   return k ? lsb(k) : -1;
 }
 
-__device__ __noinline__ bool attacked(const DBoard& b, int s, int by, uint64_t occ) {
-  const uint64_t them = b.bc[by];
-  if (pawn_att(by ^ 1, s) & b.bt[PAWN] & them) return true;
-  if (knight_att(s) & b.bt[KNIGHT] & them) return true;
-  if (king_att(s) & b.bt[KING] & them) return true;
-  if (bishop_att(s, occ) & (b.bt[BISHOP] | b.bt[QUEEN]) & them) return true;
-  if (rook_att(s, occ) & (b.bt[ROOK] | b.bt[QUEEN]) & them) return true;
-  return false;
+__device__ __forceinline__ bool attacked(const DBoard& b, int s, int by, uint64_t occ) {
+  const uint64_t them = colour(b, by);
+  return ((pawn_att(by ^ 1, s) & b.bt[PAWN]) | (knight_att(s) & b.bt[KNIGHT]) | (king_att(s) & b.bt[KING]) |
+          (bishop_att(s, occ) & (b.bt[BISHOP] | b.bt[QUEEN])) | (rook_att(s, occ) & (b.bt[ROOK] | b.bt[QUEEN]))) &
+         them;
 }
 
 // Board::do_move (board.cpp), on bitboards.
-__device__ __noinline__ void do_move(DBoard& b, const DMove& m) {
+__device__ __forceinline__ void do_move(DBoard& b, const DMove& m) {
   const int us = b.stm;
   const int pc = piece_at(b, m.from);
   const int back = us == WHITE ? 0 : 56;
@@ -129,7 +160,7 @@ __device__ __noinline__ void do_move(DBoard& b, const DMove& m) {
     remove_sq(b, m.to);
     put(b, kto, pc);
     put(b, rto, rook);
-    b.cr[us][0] = b.cr[us][1] = -1;
+    cr_clear(b, us);
   } else {
     remove_sq(b, m.to);
     if ((pc & 7) == PAWN) {
@@ -138,7 +169,7 @@ __device__ __noinline__ void do_move(DBoard& b, const DMove& m) {
     }
     remove_sq(b, m.from);
     put(b, m.to, m.promo ? make_piece_d(us, m.promo) : pc);
-    if ((pc & 7) == KING) b.cr[us][0] = b.cr[us][1] = -1;
+    if ((pc & 7) == KING) cr_clear(b, us);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -149,11 +180,35 @@ __device__ __noinline__ void do_move(DBoard& b, const DMove& m) {
   b.stm = (uint8_t)(us ^ 1);
 }
 
-__device__ __noinline__ bool legal(const DBoard& b, const DMove& m) {
+__device__ __forceinline__ bool legal(const DBoard& b, const DMove& m) {
   DBoard c = b;
   do_move(c, m);
   const int k = king_sq(c, b.stm);
   return k >= 0 && !attacked(c, k, b.stm ^ 1, c.bc[0] | c.bc[1]);
+}
+
+// Board::pseudo_moves' castling conditions for the rook on rsq (side 0 king
+// side, 1 queen side): rook in place, king on its back rank, the squares
+// between and the destinations empty, the king not in check and not passing
+// an attacked square.
+__device__ __forceinline__ bool castle_ok(const DBoard& b, int ksq, int rsq, int side) {
+  const int us = b.stm, them = us ^ 1;
+  const int back = us == WHITE ? 0 : 56;
+  const uint64_t occ = b.bc[0] | b.bc[1];
+  if (rsq < 0 || piece_at(b, rsq) != make_piece_d(us, ROOK)) return false;
+  const int kto = back + (side == 0 ? 6 : 2), rto = back + (side == 0 ? 5 : 3);
+  const int lo = min(min(ksq, rsq), min(kto, rto)), hi = max(max(ksq, rsq), max(kto, rto));
+  // [lo, hi] without the king and the rook must be empty
+  const uint64_t span = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+  if (occ & span & ~(1ull << ksq) & ~(1ull << rsq)) return false;
+  if (attacked(b, ksq, them, occ)) return false;
+  const int step = kto > ksq ? 1 : -1;
+  bool ok = true;
+  for (int t = ksq; t != kto && ok;) {
+    t += step;
+    if (attacked(b, t, them, occ)) ok = false;
+  }
+  return ok;
 }
 
 // Legal moves in the order of Board::pseudo_moves + is_legal (board.cpp):
@@ -163,7 +218,7 @@ __device__ __noinline__ bool legal(const DBoard& b, const DMove& m) {
 template <class F>
 __device__ void for_each_legal(const DBoard& b, F&& f, uint64_t from_mask = ~0ull) {
   const int us = b.stm, them = us ^ 1;
-  const uint64_t occ = b.bc[0] | b.bc[1], own = b.bc[us], opp = b.bc[them];
+  const uint64_t occ = b.bc[0] | b.bc[1], own = colour(b, us), opp = colour(b, them);
   const int up = us == WHITE ? 8 : -8;
   const int rank7 = us == WHITE ? 6 : 1, rank2 = us == WHITE ? 1 : 6;
   auto emit = [&](int from, int to, int promo, int castle) -> bool {
@@ -207,33 +262,73 @@ __device__ void for_each_legal(const DBoard& b, F&& f, uint64_t from_mask = ~0ul
   const int back = us == WHITE ? 0 : 56;
   if (ksq < 0 || (ksq & 56) != back || !((from_mask >> ksq) & 1)) return;
   for (int side = 0; side < 2; ++side) {
-    const int rsq = b.cr[us][side];
-    if (rsq < 0 || piece_at(b, rsq) != make_piece_d(us, ROOK)) continue;
-    const int kto = back + (side == 0 ? 6 : 2), rto = back + (side == 0 ? 5 : 3);
-    const int lo = min(min(ksq, rsq), min(kto, rto)), hi = max(max(ksq, rsq), max(kto, rto));
-    bool ok = true;
-    for (int t = lo; t <= hi && ok; ++t)
-      if (t != ksq && t != rsq && (occ & (1ull << t))) ok = false;
-    if (!ok || attacked(b, ksq, them, occ)) continue;
-    const int step = kto > ksq ? 1 : -1;
-    for (int t = ksq; t != kto && ok;) {
-      t += step;
-      if (attacked(b, t, them, occ)) ok = false;
-    }
-    if (ok && !emit(ksq, rsq, 0, 1)) return;  // legal() re-checks the king; castling already is
+    const int rsq = cr_get(b, us, side);
+    if (castle_ok(b, ksq, rsq, side) && !emit(ksq, rsq, 0, 1)) return;  // legal() re-checks the king
   }
 }
 
-__device__ __noinline__ fnnue_pos pack(const DBoard& b) {
-  fnnue_pos p;
+// Is m one of Board::pseudo_moves' moves?  (The set the host builder matches
+// UCI tokens against, before the legality filter.)
+__device__ __forceinline__ bool pseudo_member(const DBoard& b, const DMove& m) {
+  const int us = b.stm, them = us ^ 1;
+  const uint64_t occ = b.bc[0] | b.bc[1], own = colour(b, us), opp = colour(b, them);
+  const uint64_t fm = 1ull << m.from, tm = 1ull << m.to;
+  if (!(own & fm)) return false;
+  if (m.castle) {
+    const int ksq = king_sq(b, us), back = us == WHITE ? 0 : 56;
+    if (m.promo || m.from != ksq || (ksq & 56) != back) return false;
+    const int side = cr_get(b, us, 0) == m.to ? 0 : cr_get(b, us, 1) == m.to ? 1 : -1;
+    return side >= 0 && castle_ok(b, ksq, m.to, side);
+  }
+  const int t = type_at(b, fm);
+  if (t == PAWN) {
+    const int r = m.from >> 3, up = us == WHITE ? 8 : -8;
+    const bool promo_rank = r == (us == WHITE ? 6 : 1);
+    const bool promo_ok = promo_rank ? m.promo != 0 : m.promo == 0;
+    const int t1 = m.from + up, t2 = t1 + up;
+    bool ok = false;
+    if (!(occ & (1ull << t1))) {
+      ok = m.to == t1 && promo_ok;
+      ok = ok || (m.to == t2 && r == (us == WHITE ? 1 : 6) && !(occ & (1ull << t2)) && m.promo == 0);
+    }
+    const uint64_t pa = pawn_att(us, m.from);
+    ok = ok || ((pa & opp & tm) && promo_ok);
+    ok = ok || (b.ep >= 0 && m.to == b.ep && (pa & tm) && m.promo == 0);
+    return ok;
+  }
+  uint64_t targets;
+  if (t == KNIGHT) targets = knight_att(m.from);
+  else if (t == BISHOP) targets = bishop_att(m.from, occ);
+  else if (t == ROOK) targets = rook_att(m.from, occ);
+  else if (t == QUEEN) targets = bishop_att(m.from, occ) | rook_att(m.from, occ);
+  else targets = king_att(m.from);
+  return m.promo == 0 && (targets & ~own & tm);
+}
+
+// Packed record from the bitboards, branch-free: bit k of a square's nibble
+// is bit k of the piece code (type bits 0-2: P=1 N=2 B=3 R=4 Q=5 K=6; bit 3
+// black), so each nibble plane is an OR of type bitboards, spread from 8 bits
+// of a rank to 8 nibbles.  Board::pack on every consistent board.
+__device__ __forceinline__ uint32_t spread8(uint32_t x) {
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+
+__device__ __forceinline__ fnnue_pos pack(const DBoard& b) {
+  const uint64_t q0 = b.bt[PAWN] | b.bt[BISHOP] | b.bt[QUEEN];
+  const uint64_t q1 = b.bt[KNIGHT] | b.bt[BISHOP] | b.bt[KING];
+  const uint64_t q2 = b.bt[ROOK] | b.bt[QUEEN] | b.bt[KING];
+  const uint64_t q3 = b.bc[BLACK];
   uint32_t w[9];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) w[i] = 0;
-  for (uint64_t o = b.bc[0] | b.bc[1]; o; o &= o - 1) {
-    const int s = lsb(o);
-    w[s >> 3] |= (uint32_t)piece_at(b, s) << (4 * (s & 7));
+  for (int r = 0; r < 8; ++r) {
+    const int sh = 8 * r;
+    w[r] = spread8((uint32_t)(q0 >> sh) & 255u) | (spread8((uint32_t)(q1 >> sh) & 255u) << 1) |
+           (spread8((uint32_t)(q2 >> sh) & 255u) << 2) | (spread8((uint32_t)(q3 >> sh) & 255u) << 3);
   }
   w[8] = b.stm;
+  fnnue_pos p;
   memcpy(&p, w, sizeof(p));
   return p;
 }
@@ -336,13 +431,21 @@ __device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t en
         side = rsq > k ? 0 : 1;
         b.c960 = 1;
       }
-      if (rsq >= 0) b.cr[col][side] = (int8_t)rsq;
+      if (rsq >= 0) {
+        if (col) {
+          if (side) b.cr[1][1] = (int8_t)rsq;
+          else b.cr[1][0] = (int8_t)rsq;
+        } else {
+          if (side) b.cr[0][1] = (int8_t)rsq;
+          else b.cr[0][0] = (int8_t)rsq;
+        }
+      }
     }
   }
   for (int col = 0; col < 2; ++col) {
     const int k = king_sq(b, col);
     for (int side = 0; side < 2; ++side) {
-      const int rsq = b.cr[col][side];
+      const int rsq = cr_get(b, col, side);
       if (rsq < 0) continue;
       if ((k & 7) != 4 || ((rsq & 7) != (side == 0 ? 7 : 0))) b.c960 = 1;
     }
@@ -352,51 +455,6 @@ __device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t en
   if (elen == 2 && text[est] >= 'a' && text[est] <= 'h' && text[est + 1] >= '1' && text[est + 1] <= '8')
     b.ep = (int8_t)((text[est + 1] - '1') * 8 + (text[est] - 'a'));
   return true;
-}
-
-// parse_uci (board.cpp) on decoded squares: the legal move from `from` to
-// `to` with promotion `promo` (0 none, KNIGHT..QUEEN), castling written as
-// king-takes-rook or, in standard positions, as the king's two-square step.
-__device__ bool match_decoded(const DBoard& b, int from, int to, int promo, DMove& out) {
-  bool found = false;
-  for_each_legal(b, [&](const DMove& m) -> bool {
-    if (m.from != from || m.promo != promo) return true;
-    const bool hit = m.to == to || (m.castle && !b.c960 && to == (m.from & 56) + (m.to > m.from ? 6 : 2));
-    if (hit) {
-      out = m;
-      found = true;
-    }
-    return !hit;
-  }, 1ull << from);  // only the moving piece's moves: same order, same first match
-  return found;
-}
-
-// Packed record from the bitboards, branch-free: bit k of a square's nibble
-// is bit k of the piece code (type bits 0-2: P=1 N=2 B=3 R=4 Q=5 K=6; bit 3
-// black), so each nibble plane is an OR of type bitboards, spread from 8 bits
-// of a rank to 8 nibbles.  Equals pack() on every consistent board.
-__device__ __forceinline__ uint32_t spread8(uint32_t x) {
-  x = (x | (x << 12)) & 0x000F000Fu;
-  x = (x | (x << 6)) & 0x03030303u;
-  return (x | (x << 3)) & 0x11111111u;
-}
-
-__device__ fnnue_pos pack_fast(const DBoard& b) {
-  const uint64_t q0 = b.bt[PAWN] | b.bt[BISHOP] | b.bt[QUEEN];
-  const uint64_t q1 = b.bt[KNIGHT] | b.bt[BISHOP] | b.bt[KING];
-  const uint64_t q2 = b.bt[ROOK] | b.bt[QUEEN] | b.bt[KING];
-  const uint64_t q3 = b.bc[BLACK];
-  uint32_t w[9];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const int sh = 8 * r;
-    w[r] = spread8((uint32_t)(q0 >> sh) & 255u) | (spread8((uint32_t)(q1 >> sh) & 255u) << 1) |
-           (spread8((uint32_t)(q2 >> sh) & 255u) << 2) | (spread8((uint32_t)(q3 >> sh) & 255u) << 3);
-  }
-  w[8] = b.stm;
-  fnnue_pos p;
-  memcpy(&p, w, sizeof(p));
-  return p;
 }
 
 // Chess rules of the wave replay (replay_wave.h).
@@ -431,13 +489,13 @@ struct ChessRules {
   __device__ static bool interpret(const DBoard& b, uint32_t code, DMove& m) {
     const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
     const uint64_t fm = 1ull << from;
-    if (!(b.bc[b.stm] & fm)) return false;
+    if (!(colour(b, b.stm) & fm)) return false;
     m = DMove{from, to, promo, 0};
     if ((b.bt[KING] & fm) && !promo) {
       const int back = b.stm == WHITE ? 0 : 56;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
-        const int rsq = b.cr[b.stm][side];
+        const int rsq = cr_get(b, b.stm, side);
         if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
           m = DMove{from, rsq, 0, 1};
           return true;
@@ -447,16 +505,17 @@ struct ChessRules {
     return true;
   }
   __device__ static void do_move(DBoard& b, const DMove& m) { fnnue::do_move(b, m); }
-  __device__ static bool verify(const DBoard& b, uint32_t code, const DMove& m) {
-    DMove x;
-    return match_decoded(b, (int)replay::tok_from(code), (int)replay::tok_to(code), (int)replay::tok_piece(code), x) &&
-           x.from == m.from && x.to == m.to && x.promo == m.promo && x.castle == m.castle;
-  }
-  __device__ static fnnue_pos pack(const DBoard& b) { return pack_fast(b); }
+  // interpret() built m from the token; the host builder accepts the token iff
+  // a legal move prints as it, and that move can only be m (a castling move's
+  // destination holds the own rook or lies two files from the unmoved king,
+  // where no other move goes): so the token is accepted iff m is legal.
+  __device__ static bool verify(const DBoard& b, uint32_t, const DMove& m) { return pseudo_member(b, m) && legal(b, m); }
+  __device__ static fnnue_pos pack(const DBoard& b) { return fnnue::pack(b); }
   __device__ static bool any_legal_from(const DBoard& b, int sq, bool) {
-    if (!((b.bc[b.stm] >> sq) & 1)) return false;
+    if (!((colour(b, b.stm) >> sq) & 1)) return false;
     bool any = false;
-    for_each_legal(b, [&](const DMove&) -> bool {
+    const DBoard c = b;  // the generator takes its board by reference: a copy, so the chain's board stays in registers
+    for_each_legal(c, [&](const DMove&) -> bool {
       any = true;
       return false;
     }, 1ull << sq);

@@ -103,15 +103,21 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   const uint32_t nmoves = nply - 1;
 
   // ---- root: FEN through LDS, parsed by every lane alike ----
+  // (parsed into a temporary: a board whose address reaches an out-of-line
+  // parser lives in scratch memory, and the chain below must stay in registers)
   Board b;
   bool ok;
-  const uint32_t flen = m0 - f0;
-  if (flen <= (uint32_t)kFenLds) {
-    for (uint32_t i = lane; i < flen; i += 64) FEN[i] = text[f0 + i];
-    lds_fence();
-    ok = R::parse_fen(FEN, 0, flen, variant, b);
-  } else {
-    ok = R::parse_fen(text, f0, m0, variant, b);
+  {
+    Board parsed;
+    const uint32_t flen = m0 - f0;
+    if (flen <= (uint32_t)kFenLds) {
+      for (uint32_t i = lane; i < flen; i += 64) FEN[i] = text[f0 + i];
+      lds_fence();
+      ok = R::parse_fen(FEN, 0, flen, variant, parsed);
+    } else {
+      ok = R::parse_fen(text, f0, m0, variant, parsed);
+    }
+    b = parsed;
   }
   if (!ok) {
     if (lane == 0) latch(err, kBuildErrFen, g, 0);

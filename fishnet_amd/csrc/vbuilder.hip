@@ -93,7 +93,8 @@ struct VariantRules {
     const bool own = (b.bc[b.stm] >> sq) & 1;
     if (!own && !drops) return false;
     bool any = false;
-    vb::for_each_legal(b, [&](const vb::VMove&) -> bool {
+    const vb::VBoard c = b;  // a copy for the by-reference generator: the chain's board stays in registers
+    vb::for_each_legal(c, [&](const vb::VMove&) -> bool {
       any = true;
       return false;
     }, own ? 1ull << sq : 0ull, own, drops);

@@ -262,3 +262,67 @@ def test_concurrent_callers(chan):
     for t in range(4):
         for b, rows in zip(bodies[t * 5:(t + 1) * 5], out[t]):
             check_rows(on, b, rows)
+
+
+# Positions where a UCI token's meaning is subtle: castling both ways and in
+# Chess960 (king already on its destination, rook beside it), en passant
+# (legal, and exposing the own king), promotions with and without capture,
+# checks, pins.
+TOKEN_FENS = [
+    START,
+    "r3k2r/p1ppqpb1/bn2pnp1/3PN3/1p2P3/2N2Q1p/PPPBBPPP/R3K2R w KQkq - 0 1",
+    "r3k2r/p1ppqpb1/bn2pnp1/3PN3/Pp2P3/2N2Q1p/1PPBBPPP/R3K2R b KQkq a3 0 1",
+    "8/2p5/3p4/KP5r/1R3p1k/8/4P1P1/8 w - - 0 1",
+    "8/8/8/KPp4r/8/8/8/4k3 w - c6 0 1",
+    "r3k2r/Pppp1ppp/1b3nbN/nP6/BBP1P3/q4N2/Pp1P2PP/R2Q1RK1 w kq - 0 1",
+    "rnbq1k1r/pp1Pbppp/2p5/8/2B5/8/PPP1NnPP/RNBQK2R w KQ - 1 8",
+    "4k3/1P6/8/8/8/8/6p1/4K2R b K - 0 1",
+    C960,
+    "1rk1r3/pppppppp/8/8/8/8/PPPPPPPP/1RK1R3 w BEbe - 0 1",
+    "r5kr/pppppppp/8/8/8/8/PPPPPPPP/R5KR w HAha - 0 1",
+    "4k3/8/8/8/8/8/4q3/4K2R w K - 0 1",
+    "r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1",
+    "r3k2r/8/8/8/8/8/8/R3K2R b KQkq - 0 1",
+]
+
+
+def _stm_squares(fen):
+    pos = F.pos_from_fen(fen)
+    stm = int(pos[32])
+    sq = []
+    for s in range(64):
+        pc = (int(pos[s >> 1]) >> (4 * (s & 1))) & 15
+        if pc and (pc >> 3) == stm:
+            sq.append(s)
+    return sq
+
+
+def test_every_token_matches_the_host_builder(chan):
+    """Every from-square of the side to move x every destination x {none,
+    q, n, r, b, k, Q} as a one-move analysis batch: the device replay accepts
+    exactly the tokens the host builder (board.cpp parse_uci, perft-pinned)
+    accepts, and the position it plays to evaluates like the host's."""
+    stub, on = chan
+    name = lambda s: "abcdefgh"[s & 7] + "12345678"[s >> 3]
+    bodies, host = [], []
+    for fi, fen in enumerate(TOKEN_FENS):
+        for f in _stm_squares(fen):
+            for t in range(64):
+                for p in ("", "q", "n", "r", "b", "k", "Q"):
+                    tok = name(f) + name(t) + p
+                    try:
+                        pos = F.game_positions(fen, tok)
+                    except F.FnnueError:
+                        pos = None
+                    bodies.append(B.AcquireResponseBody(f"{fi}:{tok}", fen, tok))
+                    host.append(pos)
+    res = stub.go(bodies)
+    ok = [i for i, p in enumerate(host) if p is not None]
+    assert 200 < len(ok) < len(host)
+    for i, (b, r) in enumerate(zip(bodies, res)):
+        assert isinstance(r, B.PositionFailed) == (host[i] is None), (b.batch_id, r)
+    after = np.stack([host[i][1] for i in ok])
+    ps, po, rc = on[0].eval_packed(after, threads=8)
+    assert rc == 0
+    got = np.array([(res[i][1].psqt, res[i][1].positional) for i in ok])
+    assert np.array_equal(got[:, 0], ps) and np.array_equal(got[:, 1], po)
