@@ -125,8 +125,8 @@ int pack_checked(const vb::VBoard& b, fnnue_vpos* out) {
   int n = vb::vpopcnt(vb::occupied(b));
   for (int c = 0; c < 2; ++c)
     for (int t = 0; t < 5; ++t) {
-      if (b.hand[c][t] > kVHandSlots) return fail(FNNUE_E_FEN, "more than 16 pieces of a type in hand");
-      n += b.hand[c][t];
+      if (vb::in_hand(b, c, t + 1) > kVHandSlots) return fail(FNNUE_E_FEN, "more than 16 pieces of a type in hand");
+      n += vb::in_hand(b, c, t + 1);
     }
   if (n > 32) return fail(FNNUE_E_FEN, "more than 32 pieces on board and in hand");
   *out = vb::pack(b);

@@ -45,7 +45,7 @@ struct VBoard {
   uint64_t bc[2];     // by colour
   uint64_t bt[7];     // by piece type 1..6
   uint64_t promoted;  // crazyhouse: promoted pieces (go to the pocket as pawns)
-  uint8_t hand[2][5]; // pockets: [colour][P N B R Q]
+  uint64_t pocket[2]; // pockets: byte t - 1 of pocket[c] = colour c's pieces of type t (P N B R Q)
   int8_t cr[2][2];    // castling rook squares [colour][0 king side, 1 queen side], -1 none
   int8_t ep;          // en-passant target square or -1
   uint8_t stm;
@@ -79,38 +79,79 @@ FNNUE_HD uint64_t pawn_att(int c, int s) {  // squares a pawn of colour c on s a
   const uint64_t b = 1ull << s;
   return c == 0 ? ((b << 9) & kNotA) | ((b << 7) & kNotH) : ((b >> 7) & kNotA) | ((b >> 9) & kNotH);
 }
-FNNUE_HD uint64_t ray(int s, int dr, int df, uint64_t occ) {
-  uint64_t a = 0;
-  int r = (s >> 3) + dr, f = (s & 7) + df;
-  while (r >= 0 && r < 8 && f >= 0 && f < 8) {
-    const int t = r * 8 + f;
-    a |= 1ull << t;
-    if (occ & (1ull << t)) break;
-    r += dr;
-    f += df;
-  }
-  return a;
+// Sliding attacks by occluded fill (Kogge-Stone): a fixed instruction
+// sequence, so device lanes holding different boards never diverge.  SH > 0
+// shifts left; `mask` removes squares that wrapped around a board edge.
+template <int SH>
+FNNUE_HD uint64_t shl(uint64_t b) {
+  return SH > 0 ? b << SH : b >> -SH;
+}
+template <int SH>
+FNNUE_HD uint64_t fill(uint64_t gen, uint64_t empty, uint64_t mask) {
+  uint64_t pro = empty & mask;
+  gen |= pro & shl<SH>(gen);
+  pro &= shl<SH>(pro);
+  gen |= pro & shl<2 * SH>(gen);
+  pro &= shl<2 * SH>(pro);
+  gen |= pro & shl<4 * SH>(gen);
+  return shl<SH>(gen) & mask;
 }
 FNNUE_HD uint64_t bishop_att(int s, uint64_t occ) {
-  return ray(s, 1, 1, occ) | ray(s, 1, -1, occ) | ray(s, -1, 1, occ) | ray(s, -1, -1, occ);
+  const uint64_t g = 1ull << s, e = ~occ;
+  return fill<9>(g, e, kNotA) | fill<7>(g, e, kNotH) | fill<-7>(g, e, kNotA) | fill<-9>(g, e, kNotH);
 }
 FNNUE_HD uint64_t rook_att(int s, uint64_t occ) {
-  return ray(s, 1, 0, occ) | ray(s, -1, 0, occ) | ray(s, 0, 1, occ) | ray(s, 0, -1, occ);
+  const uint64_t g = 1ull << s, e = ~occ;
+  return fill<8>(g, e, ~0ull) | fill<-8>(g, e, ~0ull) | fill<1>(g, e, kNotA) | fill<-1>(g, e, kNotH);
+}
+
+// Board fields by a colour / piece type known only at run time: selects and
+// shifts, never a run-time array index (on the device an indexed register
+// array lives in scratch memory).
+FNNUE_HD uint64_t colour(const VBoard& b, int c) { return c ? b.bc[1] : b.bc[0]; }
+FNNUE_HD int in_hand(const VBoard& b, int c, int t) {  // t = PAWN..QUEEN
+  return (int)(((c ? b.pocket[1] : b.pocket[0]) >> (8 * (t - 1))) & 255u);
+}
+FNNUE_HD void hand_add(VBoard& b, int c, int t, int d) {  // the count stays within 0..255
+  const uint64_t delta = (uint64_t)(int64_t)d << (8 * (t - 1));
+  if (c) b.pocket[1] += delta;
+  else b.pocket[0] += delta;
+}
+FNNUE_HD int cr_get(const VBoard& b, int c, int side) {
+  return c ? (side ? b.cr[1][1] : b.cr[1][0]) : (side ? b.cr[0][1] : b.cr[0][0]);
+}
+FNNUE_HD void cr_set(VBoard& b, int c, int side, int v) {
+  if (c) {
+    if (side) b.cr[1][1] = (int8_t)v;
+    else b.cr[1][0] = (int8_t)v;
+  } else {
+    if (side) b.cr[0][1] = (int8_t)v;
+    else b.cr[0][0] = (int8_t)v;
+  }
+}
+FNNUE_HD void cr_clear(VBoard& b, int c) {
+  cr_set(b, c, 0, -1);
+  cr_set(b, c, 1, -1);
 }
 
 FNNUE_HD uint64_t occupied(const VBoard& b) { return b.bc[0] | b.bc[1]; }
 
+FNNUE_HD int type_at(const VBoard& b, uint64_t m) {  // 0: empty
+  int t = 0;
+  for (int k = 1; k <= KING; ++k) t = (b.bt[k] & m) ? k : t;
+  return t;
+}
 FNNUE_HD int piece_at(const VBoard& b, int s) {
   const uint64_t m = 1ull << s;
-  if (!(occupied(b) & m)) return 0;
-  int t = 1;
-  while (t < KING && !(b.bt[t] & m)) ++t;
-  return mkpc((b.bc[1] & m) ? 1 : 0, t);
+  const int t = type_at(b, m);
+  return t ? mkpc((b.bc[1] & m) ? 1 : 0, t) : 0;
 }
 FNNUE_HD void put(VBoard& b, int s, int pc) {
   const uint64_t m = 1ull << s;
-  b.bc[pc >> 3] |= m;
-  b.bt[pc & 7] |= m;
+  const int c = pc >> 3, t = pc & 7;
+  b.bc[0] |= c ? 0ull : m;
+  b.bc[1] |= c ? m : 0ull;
+  for (int k = 1; k <= KING; ++k) b.bt[k] |= k == t ? m : 0ull;
 }
 FNNUE_HD void remove_sq(VBoard& b, int s) {
   const uint64_t m = ~(1ull << s);
@@ -120,19 +161,16 @@ FNNUE_HD void remove_sq(VBoard& b, int s) {
   b.promoted &= m;
 }
 FNNUE_HD int king_sq(const VBoard& b, int c) {
-  const uint64_t k = b.bt[KING] & b.bc[c];
+  const uint64_t k = b.bt[KING] & colour(b, c);
   return k ? vlsb(k) : -1;
 }
 
 // Is square s attacked by colour `by` (occupancy occ)?  Plain chess attacks.
 FNNUE_HD bool attacked(const VBoard& b, int s, int by, uint64_t occ) {
-  const uint64_t them = b.bc[by];
-  if (pawn_att(by ^ 1, s) & b.bt[PAWN] & them) return true;
-  if (knight_att(s) & b.bt[KNIGHT] & them) return true;
-  if (king_att(s) & b.bt[KING] & them) return true;
-  if (bishop_att(s, occ) & (b.bt[BISHOP] | b.bt[QUEEN]) & them) return true;
-  if (rook_att(s, occ) & (b.bt[ROOK] | b.bt[QUEEN]) & them) return true;
-  return false;
+  const uint64_t them = colour(b, by);
+  return ((pawn_att(by ^ 1, s) & b.bt[PAWN]) | (knight_att(s) & b.bt[KNIGHT]) | (king_att(s) & b.bt[KING]) |
+          (bishop_att(s, occ) & (b.bt[BISHOP] | b.bt[QUEEN])) | (rook_att(s, occ) & (b.bt[ROOK] | b.bt[QUEEN]))) &
+         them;
 }
 
 // Would the side to move's king be in danger on square s?  Atomic: a king
@@ -144,7 +182,7 @@ FNNUE_HD bool king_danger(const VBoard& b, int s, int us, uint64_t occ) {
     const int kt = king_sq(b, them);
     if (kt >= 0 && (king_att(s) & (1ull << kt))) return false;
     VBoard c = b;
-    c.bt[KING] &= ~b.bc[them];  // kings do not capture in atomic
+    c.bt[KING] &= ~colour(b, them);  // kings do not capture in atomic
     return attacked(c, s, them, occ);
   }
   return attacked(b, s, them, occ);
@@ -155,7 +193,7 @@ FNNUE_HD void do_move(VBoard& b, const VMove& m) {
   int new_ep = -1;
   if (m.kind == 2) {
     put(b, m.to, mkpc(us, m.piece));
-    --b.hand[us][m.piece - 1];
+    hand_add(b, us, m.piece, -1);
   } else if (m.kind == 1) {
     const int back = us == 0 ? 0 : 56;
     const bool king_side = m.to > m.from;
@@ -166,7 +204,7 @@ FNNUE_HD void do_move(VBoard& b, const VMove& m) {
     put(b, kto, mkpc(us, KING));
     put(b, rto, mkpc(us, ROOK));
     if (rook_promoted) b.promoted |= 1ull << rto;
-    b.cr[us][0] = b.cr[us][1] = -1;
+    cr_clear(b, us);
   } else {
     const int pc = piece_at(b, m.from);
     int cap_sq = m.to;
@@ -178,7 +216,7 @@ FNNUE_HD void do_move(VBoard& b, const VMove& m) {
     if (cap) {
       if (b.variant == kCrazyhouse) {
         const int t = cap_promoted ? PAWN : (cap & 7);
-        if (b.hand[us][t - 1] < 255) ++b.hand[us][t - 1];
+        if (in_hand(b, us, t) < 255) hand_add(b, us, t, 1);
       }
       remove_sq(b, cap_sq);
     }
@@ -190,11 +228,11 @@ FNNUE_HD void do_move(VBoard& b, const VMove& m) {
       for (uint64_t nb = king_att(m.to) & occupied(b) & ~b.bt[PAWN]; nb; nb &= nb - 1) remove_sq(b, vlsb(nb));
     }
     if ((pc & 7) == PAWN && (m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
-    if ((pc & 7) == KING) b.cr[us][0] = b.cr[us][1] = -1;
+    if ((pc & 7) == KING) cr_clear(b, us);
   }
   // castling rights end with the rook (moved, captured, exploded) or the king
   for (int c = 0; c < 2; ++c) {
-    if (king_sq(b, c) < 0) b.cr[c][0] = b.cr[c][1] = -1;
+    if (king_sq(b, c) < 0) cr_clear(b, c);
     for (int side = 0; side < 2; ++side) {
       const int r = b.cr[c][side];
       if (r >= 0 && piece_at(b, r) != mkpc(c, ROOK)) b.cr[c][side] = -1;
@@ -219,6 +257,76 @@ FNNUE_HD bool legal_after(const VBoard& before, const VBoard& after) {
   return !king_danger(a, ku, us, occupied(a));
 }
 
+// Castling conditions for the rook on rsq (side 0 king side, 1 queen side):
+// rook in place, the squares between and the destinations empty, the king not
+// in danger on its square or on any square it passes (the king lifted off
+// its square for the latter).
+FNNUE_HD bool castle_ok(const VBoard& b, int ksq, int rsq, int side) {
+  const int us = b.stm;
+  const int back = us == 0 ? 0 : 56;
+  const uint64_t occ = occupied(b);
+  if (rsq < 0 || piece_at(b, rsq) != mkpc(us, ROOK)) return false;
+  const int kto = back + (side == 0 ? 6 : 2), rto = back + (side == 0 ? 5 : 3);
+  const int lo = imin(imin(ksq, rsq), imin(kto, rto)), hi = imax(imax(ksq, rsq), imax(kto, rto));
+  const uint64_t span = (hi == 63 ? ~0ull : ((1ull << (hi + 1)) - 1)) & ~((1ull << lo) - 1);
+  if (occ & span & ~(1ull << ksq) & ~(1ull << rsq)) return false;
+  if (king_danger(b, ksq, us, occ)) return false;
+  const int step = kto > ksq ? 1 : -1;
+  const uint64_t occ2 = occ & ~(1ull << ksq);
+  bool ok = true;
+  for (int t = ksq; t != kto && ok;) {
+    t += step;
+    if (king_danger(b, t, us, occ2)) ok = false;
+  }
+  return ok;
+}
+
+// Is m one of for_each_legal's candidate moves (before the legal_after
+// filter)?  Drops: a pocket piece on an empty square (pawns not on the first
+// or last rank); moves: as the generator makes them (atomic kings never
+// capture, en passant onto an empty square only, castling by castle_ok).
+FNNUE_HD bool pseudo_member(const VBoard& b, const VMove& m) {
+  const int us = b.stm, them = us ^ 1;
+  const uint64_t occ = occupied(b), own = colour(b, us), opp = colour(b, them);
+  const uint64_t tm = 1ull << m.to;
+  if (m.kind == 2) {
+    if (b.variant != kCrazyhouse || m.piece < PAWN || m.piece > QUEEN || !in_hand(b, us, m.piece)) return false;
+    uint64_t empty = ~occ;
+    if (m.piece == PAWN) empty &= ~(kRank1 | kRank8);
+    return (empty & tm) != 0;
+  }
+  const uint64_t fm = 1ull << m.from;
+  if (!(own & fm)) return false;
+  if (m.kind == 1) {
+    const int ksq = king_sq(b, us), back = us == 0 ? 0 : 56;
+    if (m.piece || m.from != ksq || (ksq & 56) != back) return false;
+    const int side = cr_get(b, us, 0) == m.to ? 0 : cr_get(b, us, 1) == m.to ? 1 : -1;
+    return side >= 0 && castle_ok(b, ksq, m.to, side);
+  }
+  const int t = type_at(b, fm);
+  if (t == PAWN) {
+    const int r = m.from >> 3, up = us == 0 ? 8 : -8;
+    const bool promo_ok = r == (us == 0 ? 6 : 1) ? m.piece != 0 : m.piece == 0;
+    const int t1 = m.from + up, t2 = t1 + up;
+    bool ok = false;
+    if (!(occ & (1ull << t1))) {
+      ok = m.to == t1 && promo_ok;
+      ok = ok || (m.to == t2 && r == (us == 0 ? 1 : 6) && !(occ & (1ull << t2)) && m.piece == 0);
+    }
+    const uint64_t pa = pawn_att(us, m.from);
+    ok = ok || ((pa & opp & tm) && promo_ok);
+    ok = ok || (b.ep >= 0 && m.to == b.ep && (pa & tm) && !(occ & tm) && m.piece == 0);
+    return ok;
+  }
+  uint64_t targets;
+  if (t == KNIGHT) targets = knight_att(m.from);
+  else if (t == BISHOP) targets = bishop_att(m.from, occ);
+  else if (t == ROOK) targets = rook_att(m.from, occ);
+  else if (t == QUEEN) targets = bishop_att(m.from, occ) | rook_att(m.from, occ);
+  else targets = king_att(m.from) & (b.variant == kAtomic ? ~opp : ~0ull);  // atomic kings never capture
+  return m.piece == 0 && (targets & ~own & tm) != 0;
+}
+
 // Legal moves: pieces by square (pawn pushes with promotions Q R B N, double
 // push, captures, en passant), castling king side then queen side, then drops
 // (crazyhouse: piece types P N B R Q, squares a1..h8).  f(move) returns false to
@@ -228,7 +336,7 @@ template <class F>
 __host__ __device__ void for_each_legal(const VBoard& b, F&& f, uint64_t from_mask = ~0ull, bool want_moves = true,
                                         bool want_drops = true) {
   const int us = b.stm, them = us ^ 1;
-  const uint64_t occ = occupied(b), own = b.bc[us], opp = b.bc[them];
+  const uint64_t occ = occupied(b), own = colour(b, us), opp = colour(b, them);
   const bool atomic = b.variant == kAtomic;
   auto emit = [&](int from, int to, int piece, int kind) -> bool {
     const VMove m{(int8_t)from, (int8_t)to, (int8_t)piece, (int8_t)kind};
@@ -277,27 +385,14 @@ __host__ __device__ void for_each_legal(const VBoard& b, F&& f, uint64_t from_ma
     const int back = us == 0 ? 0 : 56;
     if (ksq >= 0 && (ksq & 56) == back && ((from_mask >> ksq) & 1)) {
       for (int side = 0; side < 2; ++side) {
-        const int rsq = b.cr[us][side];
-        if (rsq < 0 || piece_at(b, rsq) != mkpc(us, ROOK)) continue;
-        const int kto = back + (side == 0 ? 6 : 2), rto = back + (side == 0 ? 5 : 3);
-        const int lo = imin(imin(ksq, rsq), imin(kto, rto)), hi = imax(imax(ksq, rsq), imax(kto, rto));
-        bool ok = true;
-        for (int t = lo; t <= hi && ok; ++t)
-          if (t != ksq && t != rsq && (occ & (1ull << t))) ok = false;
-        if (!ok || king_danger(b, ksq, us, occ)) continue;
-        const int step = kto > ksq ? 1 : -1;
-        const uint64_t occ2 = occ & ~(1ull << ksq);
-        for (int t = ksq; t != kto && ok;) {
-          t += step;
-          if (king_danger(b, t, us, occ2)) ok = false;
-        }
-        if (ok && !emit(ksq, rsq, 0, 1)) return;
+        const int rsq = cr_get(b, us, side);
+        if (castle_ok(b, ksq, rsq, side) && !emit(ksq, rsq, 0, 1)) return;
       }
     }
   }
   if (want_drops && b.variant == kCrazyhouse) {
     for (int pt = PAWN; pt <= QUEEN; ++pt) {
-      if (!b.hand[us][pt - 1]) continue;
+      if (!in_hand(b, us, pt)) continue;
       uint64_t empty = ~occ;
       if (pt == PAWN) empty &= ~(kRank1 | kRank8);
       for (uint64_t t = empty; t; t &= t - 1)
@@ -333,7 +428,7 @@ FNNUE_HD fnnue_vpos pack(const VBoard& b) {
     for (int k = 0; k < 4; ++k) d[4 * i + k] = (uint8_t)(w[i] >> (8 * k));
   d[32] = b.stm;
   for (int c = 0; c < 2; ++c)
-    for (int t = 0; t < 5; ++t) d[33 + 5 * c + t] = b.hand[c][t];
+    for (int t = 0; t < 5; ++t) d[33 + 5 * c + t] = (uint8_t)(b.pocket[c] >> (8 * t));
   return p;
 }
 
@@ -367,8 +462,7 @@ FNNUE_HD bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant,
   for (int i = 0; i < 2; ++i) b.bc[i] = 0;
   for (int i = 0; i < 7; ++i) b.bt[i] = 0;
   b.promoted = 0;
-  for (int c = 0; c < 2; ++c)
-    for (int t = 0; t < 5; ++t) b.hand[c][t] = 0;
+  b.pocket[0] = b.pocket[1] = 0;
   b.cr[0][0] = b.cr[0][1] = b.cr[1][0] = b.cr[1][1] = -1;
   b.ep = -1;
   b.stm = 0;
@@ -387,8 +481,8 @@ FNNUE_HD bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant,
       const int t = piece_type_of(ch);
       if (!t || t == KING || variant != kCrazyhouse) return false;
       const int col = (ch >= 'a' && ch <= 'z') ? 1 : 0;
-      if (b.hand[col][t - 1] == 255) return false;
-      ++b.hand[col][t - 1];
+      if (in_hand(b, col, t) == 255) return false;
+      hand_add(b, col, t, 1);
       continue;
     }
     if (ch == '[') {
@@ -456,13 +550,13 @@ FNNUE_HD bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant,
         side = rsq > k ? 0 : 1;
         b.c960 = 1;
       }
-      if (rsq >= 0) b.cr[col][side] = (int8_t)rsq;
+      if (rsq >= 0) cr_set(b, col, side, rsq);
     }
   }
   for (int col = 0; col < 2; ++col) {
     const int k = king_sq(b, col);
     for (int side = 0; side < 2; ++side) {
-      const int rsq = b.cr[col][side];
+      const int rsq = cr_get(b, col, side);
       if (rsq >= 0 && ((k & 7) != 4 || (rsq & 7) != (side == 0 ? 7 : 0))) b.c960 = 1;
     }
   }

@@ -65,13 +65,13 @@ struct VariantRules {
     }
     const int from = (int)replay::tok_from(code);
     const uint64_t fm = 1ull << from;
-    if (!(b.bc[b.stm] & fm)) return false;
+    if (!(vb::colour(b, b.stm) & fm)) return false;
     m = vb::VMove{(int8_t)from, (int8_t)to, (int8_t)pc, 0};
     if ((b.bt[vb::KING] & fm) && !pc) {
       const int back = b.stm == 0 ? 0 : 56;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
-        const int rsq = b.cr[b.stm][side];
+        const int rsq = vb::cr_get(b, b.stm, side);
         if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
           m = vb::VMove{(int8_t)from, (int8_t)rsq, 0, 1};
           return true;
@@ -81,16 +81,17 @@ struct VariantRules {
     return true;
   }
   __device__ static void do_move(vb::VBoard& b, const vb::VMove& m) { vb::do_move(b, m); }
-  __device__ static bool verify(const vb::VBoard& b, uint32_t code, const vb::VMove& m) {
-    vb::VMove x;
-    const bool drop = code & replay::kTokDrop;
-    const bool ok = vb::match_decoded(b, drop ? -1 : (int)replay::tok_from(code), (int)replay::tok_to(code),
-                                      (int)replay::tok_piece(code), drop, x);
-    return ok && x.from == m.from && x.to == m.to && x.piece == m.piece && x.kind == m.kind;
+  // As for chess (builder.hip ChessRules::verify): the token is accepted iff
+  // the move interpret() built from it is legal.
+  __device__ static bool verify(const vb::VBoard& b, uint32_t, const vb::VMove& m) {
+    if (!vb::pseudo_member(b, m)) return false;
+    vb::VBoard c = b;
+    vb::do_move(c, m);
+    return vb::legal_after(b, c);
   }
   __device__ static fnnue_vpos pack(const vb::VBoard& b) { return vb::pack(b); }
   __device__ static bool any_legal_from(const vb::VBoard& b, int sq, bool drops) {
-    const bool own = (b.bc[b.stm] >> sq) & 1;
+    const bool own = (vb::colour(b, b.stm) >> sq) & 1;
     if (!own && !drops) return false;
     bool any = false;
     const vb::VBoard c = b;  // a copy for the by-reference generator: the chain's board stays in registers

@@ -326,3 +326,52 @@ def test_every_token_matches_the_host_builder(chan):
     assert rc == 0
     got = np.array([(res[i][1].psqt, res[i][1].positional) for i in ok])
     assert np.array_equal(got[:, 0], ps) and np.array_equal(got[:, 1], po)
+
+
+VTOKEN_FENS = [
+    (ZH, "crazyhouse", ZH_START),
+    (ZH, "crazyhouse", "r1bqk2r/ppp2ppp/2n5/2b5/2B5/5N2/PPP2PPP/RNBQK2R[PNPnp] w KQkq - 0 1"),
+    (ZH, "crazyhouse", "4k3/1P6/8/3Pp3/8/8/6p1/R3K2R[Nn] w KQ e6 0 1"),
+    (ZH, "crazyhouse", "r3k2r/8/8/8/8/8/8/R3K2R[P] b KQkq - 0 1"),
+    (AT, "atomic", START),
+    (AT, "atomic", "rnbqkbnr/pppp1ppp/8/4p3/4P3/5N2/PPPP1PPP/RNBQKB1R b KQkq - 1 2"),
+    (AT, "atomic", "8/8/8/3pP3/8/8/3Kk3/8 w - d6 0 1"),
+    (AT, "atomic", "r3k2r/pppq1ppp/8/3pN3/8/8/PPPP1PPP/R3K2R w KQkq - 0 1"),
+]
+
+
+def test_every_variant_token_matches_the_host_builder(chan):
+    """As the chess test, for crazyhouse (drops of every piece letter on every
+    square, promotions, pockets) and atomic (explosions, king captures,
+    adjacent kings, en passant): device acceptance and the position played
+    equal vboard.h's host replay."""
+    stub, on = chan
+    name = lambda s: "abcdefgh"[s & 7] + "12345678"[s >> 3]
+    bodies, host, kinds = [], [], []
+    for fi, (variant, vname, fen) in enumerate(VTOKEN_FENS):
+        pos = F.vpos_from_fen(variant, fen)
+        stm = int(pos[32])
+        own = [s for s in range(64) if ((int(pos[s >> 1]) >> (4 * (s & 1))) & 15) and
+               (((int(pos[s >> 1]) >> (4 * (s & 1))) & 15) >> 3) == stm]
+        toks = [name(f) + name(t) + p for f in own for t in range(64) for p in ("", "q", "n", "k", "Q")]
+        if variant == ZH:
+            toks += [c + "@" + name(t) for c in "PNBRQKpq" for t in range(64)]
+        for tok in toks:
+            try:
+                p = F.game_vpositions(variant, fen, tok)
+            except F.FnnueError:
+                p = None
+            bodies.append(B.AcquireResponseBody(f"{fi}:{tok}", fen, tok, variant=vname))
+            host.append(p)
+            kinds.append(variant)
+    res = stub.go(bodies)
+    for i, (b, r) in enumerate(zip(bodies, res)):
+        assert isinstance(r, B.PositionFailed) == (host[i] is None), (b.batch_id, r)
+    for variant in (ZH, AT):
+        ok = [i for i, p in enumerate(host) if p is not None and kinds[i] == variant]
+        assert len(ok) > 50
+        after = np.stack([host[i][1] for i in ok])
+        ps, po, rc = on[variant].eval_packed(after, threads=8)
+        assert rc == 0
+        got = np.array([(res[i][1].psqt, res[i][1].positional) for i in ok])
+        assert np.array_equal(got[:, 0], ps) and np.array_equal(got[:, 1], po)
