@@ -60,6 +60,8 @@ CLOCK_HZ = 2.4e9  # spec peak engine clock
 CUS, SIMDS = 256, 1024
 VALU_PEAK = SIMDS * CLOCK_HZ / 4  # 64-bit-encoded wave64 VALU instructions/s (4 cycles each per SIMD)
 LDS_PEAK = CUS * CLOCK_HZ  # LDS-array busy cycles/s over all CUs
+I8_MFMA_PEAK = 5.0e15  # dense int8 MFMA (2x the ~2.5 PF dense BF16 rate per clock)
+MFMA_PEAK = SIMDS * CLOCK_HZ  # matrix-core busy cycles/s over all SIMDs (SQ_VALU_MFMA_BUSY_CYCLES counts cycles)
 METRIC = "NNUE positions evaluated/sec (1–8 MI355X) + % HBM roofline, bit-exact"
 PSQT_BUCKETS = 8
 MAIN_KERNEL = {("positions", "sliced"): "ft_slices_kernel", ("positions", "gather"): "ft_scratch_kernel",
@@ -182,6 +184,9 @@ def resource_fractions(c: dict, t_s: float) -> dict:
         fr["valu"] = {"achieved": c["SQ_INSTS_VALU"] / t_s, "peak": VALU_PEAK, "unit": "VALU wave-instr/s"}
     if c.get("SQ_LDS_IDX_ACTIVE"):
         fr["lds"] = {"achieved": c["SQ_LDS_IDX_ACTIVE"] / t_s, "peak": LDS_PEAK, "unit": "LDS-busy CU-cycles/s"}
+    if c.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
+        fr["mfma"] = {"achieved": c["SQ_VALU_MFMA_BUSY_CYCLES"] / t_s, "peak": MFMA_PEAK,
+                      "unit": "MFMA-busy SIMD-cycles/s"}
     if c.get("FETCH_SIZE") is not None and c.get("WRITE_SIZE") is not None:
         b = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
         fr["hbm"] = {"achieved": b / t_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "bytes": b}
@@ -829,6 +834,15 @@ def main():
             rec["fractions"] = resource_fractions(c, t_ms * 1e-3)
             rec["profiled_avg_ms"] = round((counters[name].get("avg_ns") or 0) / 1e6, 4)
         kernels[name] = rec
+    # L1 (fc_0, 16 x HD int8 MACs per position) and fc_1 (32 x 32) on int8 MFMA in stack_kernel: achieved
+    # int8 OP/s against the dense I8 matrix peak (2x BF16 per clock: ~5 POP/s, MI355X_MICROARCH.md Matrix cores)
+    if stack_avg > 0:
+        ops = 2.0 * npos * (16 * args.hd + 32 * 32)
+        kernels["stack_kernel"]["mfma_int8"] = {
+            "achieved_TOPs": round(ops / (stack_avg * 1e-3) / 1e12, 2), "peak_TOPs": I8_MFMA_PEAK / 1e12,
+            "frac": round(ops / (stack_avg * 1e-3) / I8_MFMA_PEAK, 5),
+            "note": "algorithmic int8 MACs x 2 of fc_0 + fc_1 per launch over its live time; "
+                    "fractions.mfma (if profiled) is SQ_VALU_MFMA_BUSY_CYCLES over SIMD-cycles"}
     fr = kernels[main_k].get("fractions", {})
     roofline = {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
     if fr:

@@ -14,16 +14,18 @@ namespace fnnue {
 
 __host__ __device__ inline int make_piece_d(int c, int pt) { return (c << 3) | pt; }
 
-// Board state a ply needs for move generation: bitboards, castling rooks
-// ([colour][0 king side, 1 queen side], -1 none), en-passant square.
+// Board state a ply needs for move generation: bitboards, castling rooks,
+// en-passant square, side to move.  The small fields are whole 32-bit words
+// (the replay's board chain runs on the scalar unit, which has no 8- or
+// 16-bit compares): castling rook of [colour c][side s] (0 king side, 1 queen
+// side) in byte 2c + s of `cr`, 0xFF none (accessors in builder.hip).
 struct DBoard {
   uint64_t bc[2];   // by colour
   uint64_t bt[7];   // by piece type (1..6), [0] unused
-  int8_t cr[2][2];
-  int8_t ep;
-  uint8_t stm;
-  uint8_t c960;     // castling rights need Chess960 notation (non-standard rook/king files)
-  uint8_t pad[1];
+  uint32_t cr;
+  int32_t ep;
+  uint32_t stm;
+  uint32_t c960;    // castling rights need Chess960 notation (non-standard rook/king files)
 };
 
 DBoard to_dboard(const Board& b);

@@ -92,16 +92,16 @@ struct DMove {
 
 __device__ __forceinline__ uint64_t colour(const DBoard& b, int c) { return c ? b.bc[1] : b.bc[0]; }
 
+// Castling rook square of colour c, side s (-1: none).
 __device__ __forceinline__ int cr_get(const DBoard& b, int c, int side) {
-  return c ? (side ? b.cr[1][1] : b.cr[1][0]) : (side ? b.cr[0][1] : b.cr[0][0]);
+  const uint32_t v = (b.cr >> (8 * (2 * c + side))) & 0xFFu;
+  return v == 0xFFu ? -1 : (int)v;
 }
-__device__ __forceinline__ void cr_clear(DBoard& b, int c) {
-  if (c) {
-    b.cr[1][0] = b.cr[1][1] = -1;
-  } else {
-    b.cr[0][0] = b.cr[0][1] = -1;
-  }
+__device__ __forceinline__ void cr_set(DBoard& b, int c, int side, int sq) {
+  const int sh = 8 * (2 * c + side);
+  b.cr = (b.cr & ~(0xFFu << sh)) | ((uint32_t)(sq < 0 ? 0xFF : sq) << sh);
 }
+__device__ __forceinline__ void cr_clear(DBoard& b, int c) { b.cr |= 0xFFFFu << (16 * c); }
 
 // Piece type on the square(s) of mask m (0: empty).
 __device__ __forceinline__ int type_at(const DBoard& b, uint64_t m) {
@@ -174,10 +174,10 @@ __device__ __forceinline__ void do_move(DBoard& b, const DMove& m) {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int side = 0; side < 2; ++side)
-        if (b.cr[c][side] == m.from || b.cr[c][side] == m.to) b.cr[c][side] = -1;
+        if (cr_get(b, c, side) == m.from || cr_get(b, c, side) == m.to) cr_set(b, c, side, -1);
   }
-  b.ep = (int8_t)new_ep;
-  b.stm = (uint8_t)(us ^ 1);
+  b.ep = new_ep;
+  b.stm = (uint32_t)(us ^ 1);
 }
 
 __device__ __forceinline__ bool legal(const DBoard& b, const DMove& m) {
@@ -355,7 +355,7 @@ __device__ __forceinline__ int count_tokens(const char* text, uint32_t p, uint32
 __device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t end, DBoard& b) {
   for (int i = 0; i < 2; ++i) b.bc[i] = 0;
   for (int i = 0; i < 7; ++i) b.bt[i] = 0;
-  b.cr[0][0] = b.cr[0][1] = b.cr[1][0] = b.cr[1][1] = -1;
+  b.cr = 0xFFFFFFFFu;
   b.ep = -1;
   b.stm = WHITE;
   b.c960 = 0;
@@ -431,15 +431,7 @@ __device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t en
         side = rsq > k ? 0 : 1;
         b.c960 = 1;
       }
-      if (rsq >= 0) {
-        if (col) {
-          if (side) b.cr[1][1] = (int8_t)rsq;
-          else b.cr[1][0] = (int8_t)rsq;
-        } else {
-          if (side) b.cr[0][1] = (int8_t)rsq;
-          else b.cr[0][0] = (int8_t)rsq;
-        }
-      }
+      if (rsq >= 0) cr_set(b, col, side, rsq);
     }
   }
   for (int col = 0; col < 2; ++col) {
@@ -453,7 +445,7 @@ __device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t en
   uint32_t est;
   const int elen = next_token(text, p, end, est);
   if (elen == 2 && text[est] >= 'a' && text[est] <= 'h' && text[est + 1] >= '1' && text[est + 1] <= '8')
-    b.ep = (int8_t)((text[est + 1] - '1') * 8 + (text[est] - 'a'));
+    b.ep = (text[est + 1] - '1') * 8 + (text[est] - 'a');
   return true;
 }
 
@@ -462,6 +454,7 @@ struct ChessRules {
   using Board = DBoard;
   using Move = DMove;
   using Pos = fnnue_pos;
+  __device__ static DBoard uniform(const DBoard& b) { return replay::first_lane(b); }
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int, DBoard& b) {
     return fnnue::parse_fen(t, p, e, b);
   }
@@ -627,9 +620,13 @@ DBoard to_dboard(const Board& h) {
   b.bc[1] = h.byColor[1];
   for (int t = 0; t < 7; ++t) b.bt[t] = t ? h.byType[t] : 0;
   for (int c = 0; c < 2; ++c)
-    for (int side = 0; side < 2; ++side) b.cr[c][side] = (int8_t)h.castle_rook[c][side];
-  b.ep = (int8_t)h.ep;
-  b.stm = (uint8_t)h.stm;
+    for (int side = 0; side < 2; ++side) {
+      const int sq = h.castle_rook[c][side];
+      const int sh = 8 * (2 * c + side);
+      b.cr = (b.cr & ~(0xFFu << sh)) | ((uint32_t)(sq < 0 ? 0xFF : sq) << sh);
+    }
+  b.ep = h.ep;
+  b.stm = (uint32_t)h.stm;
   b.c960 = h.chess960 ? 1 : 0;
   return b;
 }

@@ -57,6 +57,20 @@ __device__ __forceinline__ void lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// A wave-uniform copy of a trivially copyable value: every 32-bit word read
+// from the first active lane.
+template <class T>
+__device__ __forceinline__ T first_lane(const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "32-bit words");
+  uint32_t w[sizeof(T) / 4];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (unsigned i = 0; i < sizeof(T) / 4; ++i) w[i] = __builtin_amdgcn_readfirstlane(w[i]);
+  T out;
+  __builtin_memcpy(&out, w, sizeof(T));
+  return out;
+}
+
 __device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t game, uint32_t ply) {
   if (atomicCAS(&err[0], 0u, code) == 0u) {
     err[1] = game;
@@ -66,9 +80,11 @@ __device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t gam
 
 constexpr int kFenLds = 256;   // FENs up to this length are parsed from LDS
 constexpr int kTokRing = 128;  // pending move codes (<= 63 left + 32 new per 64 characters)
+constexpr int kTxt = 2048;     // move text staged in LDS at a time
 
 // Rules (builder.hip ChessRules, vbuilder.hip VariantRules):
 //   Board, Move, Pos
+//   Board uniform(const Board&)                         the board read from lane 0 (readfirstlane)
 //   bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant, Board&)
 //   uint32_t encode(const char* c, int len)             token -> code (kTokBad if malformed)
 //   bool interpret(const Board&, uint32_t code, Move&)   cheap: the move the code would be
@@ -91,6 +107,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   __shared__ Move MV[64];           // the moves (b) applied
   __shared__ uint32_t TK[kTokRing]; // pending token codes
   __shared__ char FEN[kFenLds];
+  __shared__ char TXT[kTxt];        // move text from tbase on (' ' past the game's end)
   const uint32_t g = blockIdx.x;
   const int lane = threadIdx.x;
   if (g >= ngames) return;
@@ -117,7 +134,10 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     } else {
       ok = R::parse_fen(text, f0, m0, variant, parsed);
     }
-    b = parsed;
+    // every lane parsed the same text: say so, so the chain below runs on
+    // scalar registers and scalar branches (one instruction per wave, no
+    // exec-mask bookkeeping) instead of 64 copies in vector registers
+    b = R::uniform(parsed);
   }
   if (!ok) {
     if (lane == 0) latch(err, kBuildErrFen, g, 0);
@@ -130,29 +150,39 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
 
   // ---- windows of up to 64 moves ----
   uint32_t p = m0;   // next text character to tokenise
+  uint32_t tbase = 0;  // text offset of TXT[0]
+  bool staged = false;
   char prev = ' ';   // the character before p
   uint32_t ntok = 0; // pending codes in TK[0 .. ntok)
   uint32_t done = 0; // moves played and checked
   uint32_t bad = 0;  // kBuildErr* of this game
   uint32_t bad_ply = 0;
   while (done < nmoves) {
-    // (a) tokenise until a full window is pending or the text ends
+    // (a) tokenise until a full window is pending or the text ends; the
+    // characters come from an LDS copy of the move text (kTxt at a time,
+    // loaded with independent loads), so a token's tail is an LDS read
     while (ntok < 64 && p < e) {
-      const uint32_t i = p + lane;
-      const char c = i < e ? text[i] : ' ';
+      if (!staged || p + 64 + 6 > tbase + (uint32_t)kTxt) {
+        tbase = p;
+        staged = true;
+        const uint32_t lim = min((uint32_t)kTxt, e - tbase + 72);  // the text, then spaces for any token tail
+        for (uint32_t q = lane; q < lim; q += 64) TXT[q] = tbase + q < e ? text[tbase + q] : ' ';
+        lds_fence();
+      }
+      const uint32_t i = p - tbase + lane;
+      const char c = TXT[i];
       const char cprev = (char)__shfl_up((int)c, 1, 64);
       const bool start = !space(c) && space(lane == 0 ? prev : cprev);
       const uint64_t starts = __ballot(start);
       if (start) {
         char t[6];
-        t[0] = c;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) t[q] = TXT[i + q];
         int len = 1;
         bool more = true;
 #pragma unroll
-        for (int k = 1; k < 6; ++k) {
-          const char ck = (more && i + k < e) ? text[i + k] : ' ';
-          more = more && !space(ck);
-          t[k] = ck;
+        for (int q = 1; q < 6; ++q) {
+          more = more && !space(t[q]);
           len += more ? 1 : 0;
         }
         const uint32_t code = (len == 4 || len == 5) ? R::encode(t, len) : kTokBad;
@@ -174,13 +204,14 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     if (lane == 0) S[0] = b;
     uint32_t kplay = k;
     for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t code = TK[j];
+      const uint32_t code = __builtin_amdgcn_readfirstlane(TK[j]);
       Move m;
       if ((code & kTokBad) || !R::interpret(b, code, m)) {
         kplay = j;
         break;
       }
       R::do_move(b, m);
+      b = R::uniform(b);  // (keeps the loop-carried board scalar)
       if (lane == 0) {
         S[j + 1] = b;
         MV[j] = m;

@@ -37,6 +37,7 @@ struct VariantRules {
   using Board = vb::VBoard;
   using Move = vb::VMove;
   using Pos = fnnue_vpos;
+  __device__ static vb::VBoard uniform(const vb::VBoard& b) { return replay::first_lane(b); }
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int variant, vb::VBoard& b) {
     return vb::parse_fen(t, p, e, variant, b);
   }
