@@ -352,7 +352,7 @@ __device__ __forceinline__ int count_tokens(const char* text, uint32_t p, uint32
 }
 
 // board_from_fen (board.cpp) on the device.  Returns false on malformed FEN.
-__device__ __noinline__ bool parse_fen(const char* text, uint32_t p, uint32_t end, DBoard& b) {
+__device__ __forceinline__ bool parse_fen(const char* text, uint32_t p, uint32_t end, DBoard& b) {
   for (int i = 0; i < 2; ++i) b.bc[i] = 0;
   for (int i = 0; i < 7; ++i) b.bt[i] = 0;
   b.cr = 0xFFFFFFFFu;

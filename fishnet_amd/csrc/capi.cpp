@@ -804,6 +804,15 @@ int eval_groups_dual_device(fnnue_ctx* a, fnnue_ctx* b, const fnnue_pos* d_pos, 
   pb.tiles = b->plan.tiles;
   pb.swar = b->plan.swar;
   pb.psqt_part = b->plan.psqt_part;
+  // A small net (HD <= 256) works best on units of half the plies (§4.4): it
+  // gets a unit table of its own, cut from the same sorted items into its own
+  // context's unit buffer and counter.
+  const uint32_t small_plies = seg_unit_plies(b->hd);
+  const bool own_units = small_plies != a->seg.unit_plies;
+  if (own_units) {
+    pb.units = b->plan.units;
+    pb.ctr = b->plan.ctr;
+  }
   for (size_t i0 = 0; i0 < npos; i0 += chunk) {
     const uint32_t m = (uint32_t)std::min<size_t>(chunk, npos - i0);
     std::array<hipEvent_t, 4>*ev = nullptr, *ev2 = nullptr;
@@ -814,19 +823,33 @@ int eval_groups_dual_device(fnnue_ctx* a, fnnue_ctx* b, const fnnue_pos* d_pos, 
             "segment plan launch");
     HIP_TRY(hipEventRecord(a->dual_fork, s), "hipEventRecord");
     HIP_TRY(hipStreamWaitEvent(s2, a->dual_fork, 0), "hipStreamWaitEvent");
-    if ((rc = record_event(a, ev, 1, s))) return rc;
-    HIP_TRY(launch_seg_ft(a->hd, kVariantChess, m, mode, a->ptrs, a->plan, a->seg, a->x, s), "ft_segments launch");
-    // the small net has no plan of its own: its plan phase is empty
-    if ((rc = record_event(b, ev2, 0, s2)) || (rc = record_event(b, ev2, 1, s2))) return rc;
-    HIP_TRY(launch_seg_ft(b->hd, kVariantChess, m, mode, b->ptrs, pb, a->seg, b->x, s2), "ft_segments launch");
-    if ((rc = record_event(b, ev2, 2, s2))) return rc;
-    HIP_TRY(launch_stack(b->hd, b->x, a->bucket, m, b->ptrs, d_positional2 + i0, nullptr, b->plan.psqt_part,
-                         d_psqt2 + i0, s2),
-            "stack kernel launch");
-    if ((rc = record_event(b, ev2, 3, s2))) return rc;
-    HIP_TRY(hipEventRecord(a->dual_join, s2), "hipEventRecord");
-    if ((rc = run_chunk_tail(a, m, d_positional + i0, s, ev, nullptr, a->plan.psqt_part, d_psqt + i0))) return rc;
-    HIP_TRY(hipStreamWaitEvent(s, a->dual_join, 0), "hipStreamWaitEvent");
+    // From the fork on, s must wait for s2 before returning, error or not
+    // (ADVICE r04): the next call on `a` overwrites the plan the small net's
+    // kernels on s2 read.
+    auto forked = [&]() -> int {
+      // (on the small context's stream: its unit buffer and counter are
+      // written in that context's workspace order)
+      if (own_units)
+        HIP_TRY(launch_seg_units(kVariantChess, a->plan, pb.units, pb.ctr, small_plies, s2), "segment units launch");
+      int r = record_event(a, ev, 1, s);
+      if (r) return r;
+      HIP_TRY(launch_seg_ft(a->hd, kVariantChess, m, mode, a->ptrs, a->plan, a->seg, a->x, s), "ft_segments launch");
+      // the small net has no plan of its own: its plan phase is empty
+      if ((r = record_event(b, ev2, 0, s2)) || (r = record_event(b, ev2, 1, s2))) return r;
+      HIP_TRY(launch_seg_ft(b->hd, kVariantChess, m, mode, b->ptrs, pb, a->seg, b->x, s2), "ft_segments launch");
+      if ((r = record_event(b, ev2, 2, s2))) return r;
+      HIP_TRY(launch_stack(b->hd, b->x, a->bucket, m, b->ptrs, d_positional2 + i0, nullptr, b->plan.psqt_part,
+                           d_psqt2 + i0, s2),
+              "stack kernel launch");
+      if ((r = record_event(b, ev2, 3, s2))) return r;
+      return run_chunk_tail(a, m, d_positional + i0, s, ev, nullptr, a->plan.psqt_part, d_psqt + i0);
+    };
+    rc = forked();
+    if (hipEventRecord(a->dual_join, s2) != hipSuccess || hipStreamWaitEvent(s, a->dual_join, 0) != hipSuccess) {
+      (void)hipStreamSynchronize(s2);  // no event to order by: the small net's work is done before s goes on
+      if (!rc) rc = fail(FNNUE_E_DEVICE, "dual join event failed");
+    }
+    if (rc) return rc;
   }
   return FNNUE_OK;
 }

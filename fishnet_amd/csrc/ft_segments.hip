@@ -996,6 +996,19 @@ hipError_t launch_seg_plan(int variant, const void* pos, uint32_t n, const void*
   return hipErrorInvalidValue;
 }
 
+hipError_t launch_seg_units(int variant, const SlicedPlan& P, void* units, uint32_t* ctr_out, uint32_t unit_plies,
+                            hipStream_t stream) {
+#define FNNUE_SEG_UNITS(Fs)                                                                                       \
+  hipLaunchKernelGGL((plan_scan_kernel_t<Fs::KB, SegCtr<Fs>::kNB>), dim3(1), dim3(1024), 0, stream, P.ctr,       \
+                     static_cast<int4*>(units), 0u, unit_plies, ctr_out + SegCtr<Fs>::kNUnits);                   \
+  return hipGetLastError();
+  if (variant == kVariantChess) { FNNUE_SEG_UNITS(ChessFs) }
+  if (variant == kVariantCrazyhouse) { FNNUE_SEG_UNITS(VariantFs<kVariantCrazyhouse>) }
+  if (variant == kVariantAtomic) { FNNUE_SEG_UNITS(VariantFs<kVariantAtomic>) }
+#undef FNNUE_SEG_UNITS
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_seg_ft(uint32_t hd, int variant, uint32_t n, int mode, const NetPtrs& net, const SlicedPlan& P,
                          const SegPlan& G, uint8_t* x, hipStream_t stream) {
   if (n == 0) return hipSuccess;

@@ -136,6 +136,12 @@ hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_
 // (P.ctr / units / flist and G), with its own tiles, swar flag, psqt_part, x.
 hipError_t launch_seg_plan(int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase, int mode,
                            const SlicedPlan& P, const SegPlan& G, uint8_t* bucket, uint32_t* err, hipStream_t stream);
+// A second unit table over a chunk's plan (after launch_seg_plan): units of
+// unit_plies into `units`, their count into ctr_out's unit-count slot, P's
+// counters untouched — the small net of a dual call runs its main kernel over
+// these (P.units = units, P.ctr = ctr_out) instead of the big net's units.
+hipError_t launch_seg_units(int variant, const SlicedPlan& P, void* units, uint32_t* ctr_out, uint32_t unit_plies,
+                            hipStream_t stream);
 hipError_t launch_seg_ft(uint32_t hd, int variant, uint32_t n, int mode, const NetPtrs& net, const SlicedPlan& P,
                          const SegPlan& G, uint8_t* x, hipStream_t stream);
 

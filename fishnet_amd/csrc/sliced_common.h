@@ -168,7 +168,7 @@ __host__ __device__ constexpr uint32_t seg_len_bin(uint32_t L) {
 // (profiles/r04q; an earlier A/B that called it neutral compared two identical
 // builds, see tools/exp_build.sh).
 #ifndef SEG_UNIT_PLIES
-#define SEG_UNIT_PLIES 16384
+#define SEG_UNIT_PLIES 20480
 #endif
 #ifndef SEG_UNIT_PLIES_SMALL
 #define SEG_UNIT_PLIES_SMALL 8192
@@ -180,6 +180,8 @@ constexpr uint32_t kSegUnitPlies = SEG_UNIT_PLIES;
 // Nets of at most 4 column slices (HD <= 256) get units of half the work: 2
 // slices per unit leave ~250 tasks for 256 CUs at 16384, one round whose span
 // is its longest task (config 3 at HD 128: ft_segments 0.144 -> 0.094 ms).
+// (Big nets: 20480 against 16384 / 12288: config 3 +0.9 % / -1.9 %, config
+// 4 ±0 / -0.5 %, profiles/r04n.)
 constexpr uint32_t kSegUnitPliesSmall = SEG_UNIT_PLIES_SMALL;
 __host__ __device__ constexpr uint32_t seg_unit_plies_for(uint32_t hd) {
   return hd <= 256 ? kSegUnitPliesSmall : kSegUnitPlies;
@@ -209,7 +211,8 @@ template <int KB, int NB = 33>
 __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel_t(uint32_t* __restrict__ ctr,
                                                                                   int4* __restrict__ units,
                                                                                   uint32_t unit_items,
-                                                                                  uint32_t seg_plies = 0) {
+                                                                                  uint32_t seg_plies = 0,
+                                                                                  uint32_t* __restrict__ nu_out = nullptr) {
   constexpr int kIB = KB * NB, kB = kIB + kPosBins, kO = kB, kC = 2 * kB, kNU = 3 * kB;
   auto len_bin = [](int i) { return (i % NB) / (NB / 33); };
   __shared__ uint32_t s[kB];
@@ -250,10 +253,13 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     }
   }
   __syncthreads();
-  for (int i = t; i < kB; i += 1024) {
-    ctr[kO + i] = s[i];
-    ctr[kC + i] = s[i];
-  }
+  // nu_out: a second unit table over a plan already scattered (another net's
+  // unit size): offsets and cursors stay as they are, the count goes to nu_out
+  if (!nu_out)
+    for (int i = t; i < kB; i += 1024) {
+      ctr[kO + i] = s[i];
+      ctr[kC + i] = s[i];
+    }
   // end of king block kb's items
   auto kb_end = [&](int kb) -> uint32_t { return kb == KB - 1 ? s[KB * NB - 1] + ctr[KB * NB - 1] : s[(kb + 1) * NB]; };
   if (unit_items == 0) {
@@ -285,7 +291,8 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
       ubase[t] = incl - mine;
       if (t == KB - 1) {
         ubase[KB] = incl;
-        ctr[kNU] = incl;
+        if (nu_out) *nu_out = incl;
+        else ctr[kNU] = incl;
       }
     }
     __syncthreads();
@@ -482,10 +489,11 @@ __device__ __forceinline__ const u32x4* row_addr(const char* base, uint32_t word
 }
 
 #ifndef FT_DEPTH
-#define FT_DEPTH 3
+#define FT_DEPTH 2
 #endif
 // Rows in flight per wave: the LDS queue stays fed and hipcc counts lgkmcnt
-// instead of draining it.
+// instead of draining it (2 against 3: config 2 +0.2 %, config 3 +0.5 %;
+// 4: -0.4 % / -5 %, profiles/r04n).
 constexpr int kRowDepth = 4 * FT_DEPTH;
 
 // SWAR rows (ft_slices when the net allows it, accumulator_bound in net.h):

@@ -445,7 +445,7 @@ def test_device_groups_offsets_checked_on_device(ev_cache):
 
 def test_segments_units_split_inside_king_block(ev_cache):
     """Many segments in ONE king block (the kings' start squares): far more than
-    2 x kSegUnitPlies (16384) plies of work there, so plan_scan cuts the king
+    2 x kSegUnitPlies (20480) plies of work there, so plan_scan cuts the king
     block's length bins into several units mid-bin (sliced_common.h
     build_units).  CHAIN over 5000 random games and STAR over the children of
     150 games, both against the oracle."""
@@ -455,7 +455,7 @@ def test_segments_units_split_inside_king_block(ev_cache):
         board = np.zeros((len(pos), 64), np.uint8)
         board[:, 0::2] = pos[:, :32] & 15
         board[:, 1::2] = pos[:, :32] >> 4
-        assert int((board[:, 4] == 6).sum()) > 2 * 16384  # white king on e1: one king block
+        assert int((board[:, 4] == 6).sum()) > 2 * 20480  # white king on e1: one king block
         ps, po = ev.eval_groups(pos, off, mode)
         ops, opo, rc = on.eval_packed(pos, threads=8)
         assert rc == 0

@@ -1,0 +1,29 @@
+"""Per-phase cycles of the wave replay for game 0 of a backend call, from the
+diagnostic build tools/exp/diag_replay_stamps.patch (run with
+FNNUE_LIB=exp/libfnnue_stamps.so): FEN, tokenising, the board chain, the
+per-lane check + pack, the tail, the game-end flags (s_memtime cycles)."""
+import ctypes as C
+import sys
+
+import numpy as np
+
+sys.path.insert(0, ".")
+import bench  # noqa: E402
+import fishnet_amd as F  # noqa: E402
+from fishnet_amd import _native as N  # noqa: E402
+from fishnet_amd import backend as B  # noqa: E402
+
+stub, actor = B.channel(F.Net.from_bytes(F.synthesize_net(1, 1024, 0)), 0)
+bodies = bench.lichess_batches(F, 1, 400, c960=0.0, variants=0.0)
+st = (C.c_ulonglong * 8)()
+names = ["fen", "tokenise", "chain", "check+pack", "tail", "end flags"]
+for k in (1, 64, 400):
+    rows = []
+    for _ in range(20):
+        stub.go(bodies[:k])
+        assert N.lib.fnnue_diag_replay_stamps(st) == 0
+        rows.append(list(st))
+    a = np.median(np.array(rows, dtype=np.float64), axis=0)
+    print(f"batches={k:4d} game0 moves={int(a[7])} total={a[6]:.0f} cyc  " +
+          "  ".join(f"{n}={v:.0f}" for n, v in zip(names, a[:6])), flush=True)
+actor.close()
