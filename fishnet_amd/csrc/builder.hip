@@ -458,6 +458,25 @@ struct ChessRules {
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int, DBoard& b) {
     return fnnue::parse_fen(t, p, e, b);
   }
+  __device__ static const char* start_fen(int) { return "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1"; }
+  __device__ static uint32_t start_fen_len(int) { return 56; }
+  __device__ static DBoard start_board(int) {
+    DBoard b;
+    b.bc[WHITE] = 0x000000000000FFFFull;
+    b.bc[BLACK] = 0xFFFF000000000000ull;
+    b.bt[0] = 0;
+    b.bt[PAWN] = 0x00FF00000000FF00ull;
+    b.bt[KNIGHT] = 0x4200000000000042ull;
+    b.bt[BISHOP] = 0x2400000000000024ull;
+    b.bt[ROOK] = 0x8100000000000081ull;
+    b.bt[QUEEN] = 0x0800000000000008ull;
+    b.bt[KING] = 0x1000000000000010ull;
+    b.cr = 7u | (0u << 8) | (63u << 16) | (56u << 24);  // [white][king side] h1, [white][queen side] a1, black h8, a8
+    b.ep = -1;
+    b.stm = WHITE;
+    b.c960 = 0;
+    return b;
+  }
   // "e2e4" / "e7e8q" (board.cpp's UCI: lowercase promotion letters n b r q;
   // 'k' / 'p' or anything else never names a generated move)
   __device__ static uint32_t encode(const char* c, int len) {
@@ -479,12 +498,12 @@ struct ChessRules {
   // to a castling rook's square or (standard positions) to its two-square
   // destination; everything else as written (en passant and double pushes
   // are do_move's business).  verify() decides whether it is legal.
-  __device__ static bool interpret(const DBoard& b, uint32_t code, DMove& m) {
+  __device__ static bool interpret(const DBoard& b, uint32_t code, DMove& m, uint32_t sqv) {
     const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
-    const uint64_t fm = 1ull << from;
-    if (!(colour(b, b.stm) & fm)) return false;
+    const uint32_t pc = replay::lane_value(sqv, from);
+    if (!pc || (int)(pc >> 3) != (int)b.stm) return false;
     m = DMove{from, to, promo, 0};
-    if ((b.bt[KING] & fm) && !promo) {
+    if ((pc & 7) == KING && !promo) {
       const int back = b.stm == WHITE ? 0 : 56;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
@@ -498,6 +517,44 @@ struct ChessRules {
     return true;
   }
   __device__ static void do_move(DBoard& b, const DMove& m) { fnnue::do_move(b, m); }
+  __device__ static uint32_t lane_square(const DBoard& b, int sq) { return (uint32_t)piece_at(b, sq); }
+  // do_move with lane l holding square l's piece code: every square the move
+  // changes is one select per lane; the bitboards are then the lanes' ballots.
+  __device__ static void play(DBoard& b, const DMove& m, uint32_t& sqv, int lane) {
+    const int us = b.stm;
+    const int pc = (int)replay::lane_value(sqv, m.from);
+    const int back = us == WHITE ? 0 : 56;
+    uint32_t v = sqv;
+    int new_ep = -1;
+    if (m.castle) {
+      const bool king_side = m.to > m.from;
+      const int kto = back + (king_side ? 6 : 2), rto = back + (king_side ? 5 : 3);
+      v = (lane == m.from || lane == m.to) ? 0u : v;
+      v = lane == kto ? (uint32_t)pc : v;
+      v = lane == rto ? (uint32_t)make_piece_d(us, ROOK) : v;
+      cr_clear(b, us);
+    } else {
+      const bool pawn = (pc & 7) == PAWN;
+      const int cap = (pawn && m.to == b.ep && (m.from & 7) != (m.to & 7)) ? m.to + (us == WHITE ? -8 : 8) : -1;
+      v = (lane == m.from || lane == cap) ? 0u : v;
+      v = lane == m.to ? (uint32_t)(m.promo ? make_piece_d(us, m.promo) : pc) : v;
+      if (pawn && (m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
+      if ((pc & 7) == KING) cr_clear(b, us);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int side = 0; side < 2; ++side)
+          if (cr_get(b, c, side) == m.from || cr_get(b, c, side) == m.to) cr_set(b, c, side, -1);
+    }
+    sqv = v;
+    const uint32_t t = v & 7u;
+    b.bc[0] = __ballot(v != 0 && v < 8);
+    b.bc[1] = __ballot(v >= 8);
+#pragma unroll
+    for (int k = 1; k <= KING; ++k) b.bt[k] = __ballot(t == (uint32_t)k);
+    b.ep = new_ep;
+    b.stm = (uint32_t)(us ^ 1);
+  }
   // interpret() built m from the token; the host builder accepts the token iff
   // a legal move prints as it, and that move can only be m (a castling move's
   // destination holds the own rook or lies two files from the unmoved king,

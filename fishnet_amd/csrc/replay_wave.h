@@ -57,6 +57,24 @@ __device__ __forceinline__ void lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Lane `l`'s value of v, l wave-uniform (a scalar register read).
+__device__ __forceinline__ uint32_t lane_value(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+
+// v held in vector registers: the compiler treats a value read from one LDS
+// address by every lane as uniform and moves it to scalar registers, which
+// the per-lane move generation around it then exhausts (spilling to lanes).
+template <class T>
+__device__ __forceinline__ T in_vgprs(const T& v) {
+  static_assert(sizeof(T) % 4 == 0, "32-bit words");
+  uint32_t w[sizeof(T) / 4];
+  __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+  for (unsigned i = 0; i < sizeof(T) / 4; ++i) asm volatile("" : "+v"(w[i]));
+  T out;
+  __builtin_memcpy(&out, w, sizeof(T));
+  return out;
+}
+
 // A wave-uniform copy of a trivially copyable value: every 32-bit word read
 // from the first active lane.
 template <class T>
@@ -78,7 +96,6 @@ __device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t gam
   }
 }
 
-constexpr int kFenLds = 256;   // FENs up to this length are parsed from LDS
 constexpr int kTokRing = 128;  // pending move codes (<= 63 left + 32 new per 64 characters)
 constexpr int kTxt = 2048;     // move text staged in LDS at a time
 
@@ -86,9 +103,14 @@ constexpr int kTxt = 2048;     // move text staged in LDS at a time
 //   Board, Move, Pos
 //   Board uniform(const Board&)                         the board read from lane 0 (readfirstlane)
 //   bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant, Board&)
+//   const char* start_fen(int variant), uint32_t start_fen_len(int variant), Board start_board(int variant)
+//                                                       the standard start (< 64 characters) and its board
 //   uint32_t encode(const char* c, int len)             token -> code (kTokBad if malformed)
-//   bool interpret(const Board&, uint32_t code, Move&)   cheap: the move the code would be
+//   bool interpret(const Board&, uint32_t code, Move&, uint32_t sqv)  cheap: the move the code would be
+//                                                       (the board's scalar fields + the lane bytes only)
 //   void do_move(Board&, const Move&)
+//   uint32_t lane_square(const Board&, int sq)          the byte lane sq holds for the chain
+//   void play(Board&, const Move&, uint32_t& sqv, int lane)  do_move on the lane bytes + ballots
 //   bool verify(const Board&, uint32_t code, const Move&) the code matches exactly this legal move
 //   Pos pack(const Board&)
 //   bool any_legal_from(const Board&, int sq, bool drops) legal moves of the piece on sq (+ drops)
@@ -106,7 +128,6 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   __shared__ Board S[65];           // S[0]: board before the window, S[j + 1]: after its move j
   __shared__ Move MV[64];           // the moves (b) applied
   __shared__ uint32_t TK[kTokRing]; // pending token codes
-  __shared__ char FEN[kFenLds];
   __shared__ char TXT[kTxt];        // move text from tbase on (' ' past the game's end)
   const uint32_t g = blockIdx.x;
   const int lane = threadIdx.x;
@@ -125,14 +146,23 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   Board b;
   bool ok;
   {
+    // The FEN goes through the move-text buffer (free until tokenising
+    // starts); one longer than it (kTxt characters: a legal FEN has < 100)
+    // is rejected as unparsable.
     Board parsed;
     const uint32_t flen = m0 - f0;
-    if (flen <= (uint32_t)kFenLds) {
-      for (uint32_t i = lane; i < flen; i += 64) FEN[i] = text[f0 + i];
+    ok = flen <= (uint32_t)kTxt;
+    if (ok) {
+      for (uint32_t i = lane; i < flen; i += 64) TXT[i] = text[f0 + i];
       lds_fence();
-      ok = R::parse_fen(FEN, 0, flen, variant, parsed);
-    } else {
-      ok = R::parse_fen(text, f0, m0, variant, parsed);
+      // Most games start from the variant's standard position: recognised
+      // by one lane-parallel compare, its board is a constant (the parser's
+      // own result, tests/test_gpu_builder.py); any other FEN is parsed.
+      const char* sf = R::start_fen(variant);
+      const uint32_t sl = R::start_fen_len(variant);
+      const bool same = flen == sl && __ballot((uint32_t)lane < sl && TXT[lane] != sf[lane]) == 0;
+      if (same) parsed = R::start_board(variant);
+      else ok = R::parse_fen(TXT, 0, flen, variant, parsed);
     }
     // every lane parsed the same text: say so, so the chain below runs on
     // scalar registers and scalar branches (one instruction per wave, no
@@ -146,7 +176,14 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   if (lane == 0) {
     if (out) out[o0] = R::pack(b);
     if (states) states[o0] = b;
+    S[0] = b;
   }
+  // The chain keeps the board as lane bytes: lane l holds square l's piece
+  // (sqv), where a move is a handful of lane-parallel selects, and `b` only
+  // its scalar fields (side to move, castling rooks, en passant); each ply's
+  // bitboards are ballots of the lanes, stored to LDS at once (never carried
+  // from ply to ply in registers).  S[0] is the board before the window.
+  uint32_t sqv = R::lane_square(b, lane);
 
   // ---- windows of up to 64 moves ----
   uint32_t p = m0;   // next text character to tokenise
@@ -200,18 +237,16 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
       break;
     }
     const uint32_t k = min(min(ntok, 64u), nmoves - done);
-    // (b) the chain: interpret and play each move, boards to LDS
-    if (lane == 0) S[0] = b;
+    // (b) the chain: interpret and play each move (wave-uniform), boards to LDS
     uint32_t kplay = k;
     for (uint32_t j = 0; j < k; ++j) {
       const uint32_t code = __builtin_amdgcn_readfirstlane(TK[j]);
       Move m;
-      if ((code & kTokBad) || !R::interpret(b, code, m)) {
+      if ((code & kTokBad) || !R::interpret(b, code, m, sqv)) {
         kplay = j;
         break;
       }
-      R::do_move(b, m);
-      b = R::uniform(b);  // (keeps the loop-carried board scalar)
+      R::play(b, m, sqv, lane);
       if (lane == 0) {
         S[j + 1] = b;
         MV[j] = m;
@@ -239,6 +274,10 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     }
     done += k;
     ntok -= k;
+    // the next window starts from the board after this one's last move
+    static_assert(sizeof(Board) % 4 == 0 && sizeof(Board) <= 256, "board copy by dwords");
+    if ((uint32_t)lane < sizeof(Board) / 4)
+      reinterpret_cast<uint32_t*>(&S[0])[lane] = reinterpret_cast<const uint32_t*>(&S[k])[lane];
     // drop the consumed codes
     uint32_t keep[2];
 #pragma unroll
@@ -272,8 +311,10 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     return;
   }
   if (final) {
-    const bool any = __ballot(R::any_legal_from(b, lane, lane == 0)) != 0;
-    if (lane == 0) final[g] = R::end_flags(b, any);
+    lds_fence();
+    const Board last = in_vgprs(S[0]);
+    const bool any = __ballot(R::any_legal_from(last, lane, lane == 0)) != 0;
+    if (lane == 0) final[g] = R::end_flags(last, any);
   }
 }
 

@@ -41,6 +41,34 @@ struct VariantRules {
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int variant, vb::VBoard& b) {
     return vb::parse_fen(t, p, e, variant, b);
   }
+  __device__ static const char* start_fen(int variant) {
+    return variant == vb::kCrazyhouse ? "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR[] w KQkq - 0 1"
+                                      : "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1";
+  }
+  __device__ static uint32_t start_fen_len(int variant) { return variant == vb::kCrazyhouse ? 58 : 56; }
+  __device__ static vb::VBoard start_board(int variant) {
+    vb::VBoard b;
+    b.bc[0] = 0x000000000000FFFFull;
+    b.bc[1] = 0xFFFF000000000000ull;
+    b.bt[0] = 0;
+    b.bt[vb::PAWN] = 0x00FF00000000FF00ull;
+    b.bt[vb::KNIGHT] = 0x4200000000000042ull;
+    b.bt[vb::BISHOP] = 0x2400000000000024ull;
+    b.bt[vb::ROOK] = 0x8100000000000081ull;
+    b.bt[vb::QUEEN] = 0x0800000000000008ull;
+    b.bt[vb::KING] = 0x1000000000000010ull;
+    b.promoted = 0;
+    b.pocket[0] = b.pocket[1] = 0;
+    b.cr[0][0] = 7;
+    b.cr[0][1] = 0;
+    b.cr[1][0] = 63;
+    b.cr[1][1] = 56;
+    b.ep = -1;
+    b.stm = 0;
+    b.variant = (uint8_t)variant;
+    b.c960 = 0;
+    return b;
+  }
   // vb::match_uci's token rules: drops "P@e4" (piece letter either case, no
   // king), moves "e2e4" / "e7e8q" (promotion letter either case, N B R Q)
   __device__ static uint32_t encode(const char* c, int len) {
@@ -58,17 +86,17 @@ struct VariantRules {
     }
     return (uint32_t)from | ((uint32_t)to << 6) | ((uint32_t)promo << 12);
   }
-  __device__ static bool interpret(const vb::VBoard& b, uint32_t code, vb::VMove& m) {
+  __device__ static bool interpret(const vb::VBoard& b, uint32_t code, vb::VMove& m, uint32_t sqv) {
     const int to = (int)replay::tok_to(code), pc = (int)replay::tok_piece(code);
     if (code & replay::kTokDrop) {
       m = vb::VMove{-1, (int8_t)to, (int8_t)pc, 2};
       return true;
     }
     const int from = (int)replay::tok_from(code);
-    const uint64_t fm = 1ull << from;
-    if (!(vb::colour(b, b.stm) & fm)) return false;
+    const uint32_t own = replay::lane_value(sqv, from) & 15u;
+    if (!own || (int)(own >> 3) != (int)b.stm) return false;
     m = vb::VMove{(int8_t)from, (int8_t)to, (int8_t)pc, 0};
-    if ((b.bt[vb::KING] & fm) && !pc) {
+    if ((own & 7u) == (uint32_t)vb::KING && !pc) {
       const int back = b.stm == 0 ? 0 : 56;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
@@ -82,6 +110,73 @@ struct VariantRules {
     return true;
   }
   __device__ static void do_move(vb::VBoard& b, const vb::VMove& m) { vb::do_move(b, m); }
+  // lane byte: piece code, bit 4 = promoted (crazyhouse)
+  __device__ static uint32_t lane_square(const vb::VBoard& b, int sq) {
+    return (uint32_t)vb::piece_at(b, sq) | ((uint32_t)((b.promoted >> sq) & 1) << 4);
+  }
+  // vb::do_move with lane l holding square l (see ChessRules::play): drops,
+  // castling (the rook keeps its promoted mark), captures to the pocket (a
+  // promoted piece as a pawn), atomic explosions as one select per lane.
+  __device__ static void play(vb::VBoard& b, const vb::VMove& m, uint32_t& sqv, int lane) {
+    using namespace vb;
+    constexpr int PAWN = vb::PAWN, ROOK = vb::ROOK, KING = vb::KING;
+    const int us = b.stm;
+    uint32_t v = sqv;
+    int new_ep = -1;
+    if (m.kind == 2) {
+      v = lane == m.to ? (uint32_t)mkpc(us, m.piece) : v;
+      hand_add(b, us, m.piece, -1);
+    } else if (m.kind == 1) {
+      const int back = us == 0 ? 0 : 56;
+      const bool king_side = m.to > m.from;
+      const int kto = back + (king_side ? 6 : 2), rto = back + (king_side ? 5 : 3);
+      const uint32_t rook_flag = replay::lane_value(v, m.to) & 16u;
+      v = (lane == m.from || lane == m.to) ? 0u : v;
+      v = lane == kto ? (uint32_t)mkpc(us, KING) : v;
+      v = lane == rto ? ((uint32_t)mkpc(us, ROOK) | rook_flag) : v;
+      cr_clear(b, us);
+    } else {
+      const uint32_t moved = replay::lane_value(v, m.from);
+      const int pc = (int)(moved & 15u);
+      int cap_sq = m.to;
+      if ((pc & 7) == PAWN && m.to == b.ep && ((m.from ^ m.to) & 7) && !(replay::lane_value(v, m.to) & 15u))
+        cap_sq = m.to + (us == 0 ? -8 : 8);
+      const uint32_t capv = replay::lane_value(v, cap_sq);
+      const int cap = (int)(capv & 15u);
+      const bool zh = b.variant == kCrazyhouse;
+      if (cap && zh) {
+        const int t = (capv & 16u) ? PAWN : (cap & 7);
+        if (in_hand(b, us, t) < 255) hand_add(b, us, t, 1);
+      }
+      const uint32_t flag = (zh && (m.piece || (moved & 16u))) ? 16u : 0u;
+      v = (lane == m.from || (cap && lane == cap_sq)) ? 0u : v;
+      v = lane == m.to ? ((uint32_t)(m.piece ? mkpc(us, m.piece) : pc) | flag) : v;
+      if (cap && b.variant == kAtomic) {
+        // the capturer explodes with its victim, and every non-pawn around
+        const bool near = (king_att(m.to) >> lane) & 1;
+        v = (lane == m.to || (near && v != 0 && (v & 7u) != (uint32_t)PAWN)) ? 0u : v;
+      }
+      if ((pc & 7) == PAWN && (m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
+      if ((pc & 7) == KING) cr_clear(b, us);
+    }
+    sqv = v;
+    const uint32_t t = v & 7u;
+    b.bc[0] = __ballot(v != 0 && (v & 15u) < 8);
+    b.bc[1] = __ballot((v & 15u) >= 8);
+#pragma unroll
+    for (int k = 1; k <= KING; ++k) b.bt[k] = __ballot(t == (uint32_t)k);
+    b.promoted = __ballot((v & 16u) != 0);
+    // castling rights end with the rook (moved, captured, exploded) or the king
+    for (int c = 0; c < 2; ++c) {
+      if (!(b.bt[KING] & colour(b, c))) cr_clear(b, c);
+      for (int side = 0; side < 2; ++side) {
+        const int r = cr_get(b, c, side);
+        if (r >= 0 && (replay::lane_value(v, r) & 15u) != (uint32_t)mkpc(c, ROOK)) cr_set(b, c, side, -1);
+      }
+    }
+    b.ep = (int8_t)new_ep;
+    b.stm = (uint8_t)(us ^ 1);
+  }
   // As for chess (builder.hip ChessRules::verify): the token is accepted iff
   // the move interpret() built from it is legal.
   __device__ static bool verify(const vb::VBoard& b, uint32_t, const vb::VMove& m) {
