@@ -64,7 +64,8 @@ __device__ __forceinline__ uint64_t pawn_att(int c, int s) {
 // left; `mask` removes squares that wrapped around a board edge.
 template <int SH>
 __device__ __forceinline__ uint64_t shl(uint64_t b) {
-  return SH > 0 ? b << SH : b >> -SH;
+  if constexpr (SH > 0) return b << SH;
+  else return b >> -SH;
 }
 template <int SH>
 __device__ __forceinline__ uint64_t fill(uint64_t gen, uint64_t empty, uint64_t mask) {
@@ -454,7 +455,13 @@ struct ChessRules {
   using Board = DBoard;
   using Move = DMove;
   using Pos = fnnue_pos;
-  __device__ static DBoard uniform(const DBoard& b) { return replay::first_lane(b); }
+  // the board's non-square state: castling rooks (DBoard::cr packing), en passant, side to move
+  struct Scalars {
+    uint32_t cr;
+    int32_t ep;
+    uint32_t stm;
+    uint32_t c960;
+  };
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int, DBoard& b) {
     return fnnue::parse_fen(t, p, e, b);
   }
@@ -494,11 +501,16 @@ struct ChessRules {
     }
     return (uint32_t)from | ((uint32_t)to << 6) | (promo << 12);
   }
+  __device__ static Scalars scalars(const DBoard& b) { return Scalars{b.cr, b.ep, b.stm, b.c960}; }
+  __device__ static int sc_cr(uint32_t cr, int c, int side) {
+    const uint32_t v = (cr >> (8 * (2 * c + side))) & 0xFFu;
+    return v == 0xFFu ? -1 : (int)v;
+  }
   // The move the code names if it names one: castling when the own king goes
   // to a castling rook's square or (standard positions) to its two-square
   // destination; everything else as written (en passant and double pushes
   // are do_move's business).  verify() decides whether it is legal.
-  __device__ static bool interpret(const DBoard& b, uint32_t code, DMove& m, uint32_t sqv) {
+  __device__ static bool interpret(const Scalars& b, uint32_t code, DMove& m, uint32_t sqv) {
     const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
     const uint32_t pc = replay::lane_value(sqv, from);
     if (!pc || (int)(pc >> 3) != (int)b.stm) return false;
@@ -507,7 +519,7 @@ struct ChessRules {
       const int back = b.stm == WHITE ? 0 : 56;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
-        const int rsq = cr_get(b, b.stm, side);
+        const int rsq = sc_cr(b.cr, b.stm, side);
         if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
           m = DMove{from, rsq, 0, 1};
           return true;
@@ -516,11 +528,10 @@ struct ChessRules {
     }
     return true;
   }
-  __device__ static void do_move(DBoard& b, const DMove& m) { fnnue::do_move(b, m); }
   __device__ static uint32_t lane_square(const DBoard& b, int sq) { return (uint32_t)piece_at(b, sq); }
   // do_move with lane l holding square l's piece code: every square the move
-  // changes is one select per lane; the bitboards are then the lanes' ballots.
-  __device__ static void play(DBoard& b, const DMove& m, uint32_t& sqv, int lane) {
+  // changes is one select per lane, the rest is the scalars.
+  __device__ static void play(Scalars& b, const DMove& m, uint32_t& sqv, int lane) {
     const int us = b.stm;
     const int pc = (int)replay::lane_value(sqv, m.from);
     const int back = us == WHITE ? 0 : 56;
@@ -532,34 +543,68 @@ struct ChessRules {
       v = (lane == m.from || lane == m.to) ? 0u : v;
       v = lane == kto ? (uint32_t)pc : v;
       v = lane == rto ? (uint32_t)make_piece_d(us, ROOK) : v;
-      cr_clear(b, us);
+      b.cr |= 0xFFFFu << (16 * us);
     } else {
       const bool pawn = (pc & 7) == PAWN;
       const int cap = (pawn && m.to == b.ep && (m.from & 7) != (m.to & 7)) ? m.to + (us == WHITE ? -8 : 8) : -1;
       v = (lane == m.from || lane == cap) ? 0u : v;
       v = lane == m.to ? (uint32_t)(m.promo ? make_piece_d(us, m.promo) : pc) : v;
       if (pawn && (m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
-      if ((pc & 7) == KING) cr_clear(b, us);
+      if ((pc & 7) == KING) b.cr |= 0xFFFFu << (16 * us);
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int side = 0; side < 2; ++side)
-          if (cr_get(b, c, side) == m.from || cr_get(b, c, side) == m.to) cr_set(b, c, side, -1);
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t r = (b.cr >> (8 * i)) & 0xFFu;
+        if (r == (uint32_t)m.from || r == (uint32_t)m.to) b.cr |= 0xFFu << (8 * i);
+      }
     }
     sqv = v;
-    const uint32_t t = v & 7u;
-    b.bc[0] = __ballot(v != 0 && v < 8);
-    b.bc[1] = __ballot(v >= 8);
-#pragma unroll
-    for (int k = 1; k <= KING; ++k) b.bt[k] = __ballot(t == (uint32_t)k);
     b.ep = new_ep;
     b.stm = (uint32_t)(us ^ 1);
+  }
+  __device__ static uint32_t pack_move(const DMove& m) {
+    return (uint32_t)m.from | ((uint32_t)m.to << 6) | ((uint32_t)m.promo << 12) | ((uint32_t)m.castle << 15);
+  }
+  __device__ static DMove unpack_move(uint32_t w) {
+    return DMove{(int)(w & 63), (int)((w >> 6) & 63), (int)((w >> 12) & 7), (int)((w >> 15) & 1)};
+  }
+  // A snapshot's bytes (piece codes) as bitboards: bit k of a code is bitboard
+  // plane k (type bits 0-2: P=1 N=2 B=3 R=4 Q=5 K=6; bit 3 black).
+  __device__ static DBoard board_from(const uint32_t (&w)[16], const Scalars& sc) {
+    const uint64_t p0 = replay::byte_plane(w, 0), p1 = replay::byte_plane(w, 1), p2 = replay::byte_plane(w, 2);
+    const uint64_t p3 = replay::byte_plane(w, 3);
+    const uint64_t occ = p0 | p1 | p2;
+    DBoard b;
+    b.bc[WHITE] = occ & ~p3;
+    b.bc[BLACK] = occ & p3;
+    b.bt[0] = 0;
+    b.bt[PAWN] = p0 & ~p1 & ~p2;
+    b.bt[KNIGHT] = ~p0 & p1 & ~p2;
+    b.bt[BISHOP] = p0 & p1 & ~p2;
+    b.bt[ROOK] = ~p0 & ~p1 & p2;
+    b.bt[QUEEN] = p0 & ~p1 & p2;
+    b.bt[KING] = ~p0 & p1 & p2;
+    b.cr = sc.cr;
+    b.ep = sc.ep;
+    b.stm = sc.stm;
+    b.c960 = sc.c960;
+    return b;
+  }
+  __device__ static fnnue_pos pack_from(const uint32_t (&w)[16], const Scalars& sc) {
+    uint32_t q[9];
+    uint32_t nib[8];
+    replay::pack_nibbles(w, nib);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = nib[i];
+    q[8] = sc.stm;
+    fnnue_pos p;
+    memcpy(&p, q, sizeof(p));
+    return p;
   }
   // interpret() built m from the token; the host builder accepts the token iff
   // a legal move prints as it, and that move can only be m (a castling move's
   // destination holds the own rook or lies two files from the unmoved king,
   // where no other move goes): so the token is accepted iff m is legal.
-  __device__ static bool verify(const DBoard& b, uint32_t, const DMove& m) { return pseudo_member(b, m) && legal(b, m); }
+  __device__ static bool verify(const DBoard& b, const DMove& m) { return pseudo_member(b, m) && legal(b, m); }
   __device__ static fnnue_pos pack(const DBoard& b) { return fnnue::pack(b); }
   __device__ static bool any_legal_from(const DBoard& b, int sq, bool) {
     if (!((colour(b, b.stm) >> sq) & 1)) return false;

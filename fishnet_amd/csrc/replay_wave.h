@@ -99,19 +99,51 @@ __device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t gam
 constexpr int kTokRing = 128;  // pending move codes (<= 63 left + 32 new per 64 characters)
 constexpr int kTxt = 2048;     // move text staged in LDS at a time
 
+// Bit k of every byte of a 64-byte board snapshot (byte s = square s), as a
+// bitboard: the lane-parallel form of a board the chain keeps, turned back
+// into bitboards by each checking lane.
+__device__ __forceinline__ uint64_t byte_plane(const uint32_t (&w)[16], int k) {
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    uint32_t x = (w[i] >> k) & 0x01010101u;
+    x |= x >> 7;
+    x |= x >> 14;
+    x &= 0xFu;  // bit j = byte j of dword i
+    if (i < 8) lo |= x << (4 * i);
+    else hi |= x << (4 * (i - 8));
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// The 64 nibbles of fnnue_pos / fnnue_vpos (square s in nibble s) from the
+// snapshot's piece codes (low nibble of each byte).
+__device__ __forceinline__ void pack_nibbles(const uint32_t (&w)[16], uint32_t (&out)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t a = w[2 * i] & 0x0F0F0F0Fu, c = w[2 * i + 1] & 0x0F0F0F0Fu;
+    a = (a | (a >> 4)) & 0x00FF00FFu;
+    c = (c | (c >> 4)) & 0x00FF00FFu;
+    a = (a | (a >> 8)) & 0xFFFFu;
+    c = (c | (c >> 8)) & 0xFFFFu;
+    out[i] = a | (c << 16);
+  }
+}
+
 // Rules (builder.hip ChessRules, vbuilder.hip VariantRules):
-//   Board, Move, Pos
-//   Board uniform(const Board&)                         the board read from lane 0 (readfirstlane)
+//   Board, Move, Pos, Scalars (the board's non-square state, whole dwords)
 //   bool parse_fen(const char* text, uint32_t p, uint32_t end, int variant, Board&)
 //   const char* start_fen(int variant), uint32_t start_fen_len(int variant), Board start_board(int variant)
 //                                                       the standard start (< 64 characters) and its board
 //   uint32_t encode(const char* c, int len)             token -> code (kTokBad if malformed)
-//   bool interpret(const Board&, uint32_t code, Move&, uint32_t sqv)  cheap: the move the code would be
-//                                                       (the board's scalar fields + the lane bytes only)
-//   void do_move(Board&, const Move&)
-//   uint32_t lane_square(const Board&, int sq)          the byte lane sq holds for the chain
-//   void play(Board&, const Move&, uint32_t& sqv, int lane)  do_move on the lane bytes + ballots
-//   bool verify(const Board&, uint32_t code, const Move&) the code matches exactly this legal move
+//   Scalars scalars(const Board&); uint32_t lane_square(const Board&, int sq)
+//   bool interpret(const Scalars&, uint32_t code, Move&, uint32_t sqv)
+//                                                       cheap: the move the code would be
+//   void play(Scalars&, const Move&, uint32_t& sqv, int lane)  do_move on the lane bytes
+//   uint32_t pack_move(const Move&); Move unpack_move(uint32_t)
+//   Board board_from(const uint32_t (&w)[16], const Scalars&)   snapshot -> board (per lane)
+//   Pos pack_from(const uint32_t (&w)[16], const Scalars&)      snapshot -> record (per lane)
+//   bool verify(const Board&, const Move&)              the move interpret() built is legal
 //   Pos pack(const Board&)
 //   bool any_legal_from(const Board&, int sq, bool drops) legal moves of the piece on sq (+ drops)
 //   uint8_t end_flags(const Board&, bool any)             kFinal* of a last position
@@ -125,10 +157,12 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
                                                          uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
   using Board = typename R::Board;
   using Move = typename R::Move;
-  __shared__ Board S[65];           // S[0]: board before the window, S[j + 1]: after its move j
-  __shared__ Move MV[64];           // the moves (b) applied
-  __shared__ uint32_t TK[kTokRing]; // pending token codes
-  __shared__ char TXT[kTxt];        // move text from tbase on (' ' past the game's end)
+  using Sc = typename R::Scalars;
+  constexpr int kScw = sizeof(Sc) / 4;
+  static_assert(sizeof(Sc) % 4 == 0, "scalars as dwords");
+  __shared__ uint32_t SNAP[65][16];  // byte s of SNAP[j] = square s before the window's move j
+  __shared__ uint32_t TK[kTokRing];  // pending token codes
+  __shared__ char TXT[kTxt];         // move text from tbase on (' ' past the game's end)
   const uint32_t g = blockIdx.x;
   const int lane = threadIdx.x;
   if (g >= ngames) return;
@@ -141,15 +175,12 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   const uint32_t nmoves = nply - 1;
 
   // ---- root: FEN through LDS, parsed by every lane alike ----
-  // (parsed into a temporary: a board whose address reaches an out-of-line
-  // parser lives in scratch memory, and the chain below must stay in registers)
-  Board b;
+  Board root;
   bool ok;
   {
     // The FEN goes through the move-text buffer (free until tokenising
     // starts); one longer than it (kTxt characters: a legal FEN has < 100)
     // is rejected as unparsable.
-    Board parsed;
     const uint32_t flen = m0 - f0;
     ok = flen <= (uint32_t)kTxt;
     if (ok) {
@@ -161,29 +192,26 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
       const char* sf = R::start_fen(variant);
       const uint32_t sl = R::start_fen_len(variant);
       const bool same = flen == sl && __ballot((uint32_t)lane < sl && TXT[lane] != sf[lane]) == 0;
-      if (same) parsed = R::start_board(variant);
-      else ok = R::parse_fen(TXT, 0, flen, variant, parsed);
+      if (same) root = R::start_board(variant);
+      else ok = R::parse_fen(TXT, 0, flen, variant, root);
     }
-    // every lane parsed the same text: say so, so the chain below runs on
-    // scalar registers and scalar branches (one instruction per wave, no
-    // exec-mask bookkeeping) instead of 64 copies in vector registers
-    b = R::uniform(parsed);
   }
   if (!ok) {
     if (lane == 0) latch(err, kBuildErrFen, g, 0);
     return;
   }
   if (lane == 0) {
-    if (out) out[o0] = R::pack(b);
-    if (states) states[o0] = b;
-    S[0] = b;
+    if (out) out[o0] = R::pack(root);
+    if (states) states[o0] = root;
   }
-  // The chain keeps the board as lane bytes: lane l holds square l's piece
-  // (sqv), where a move is a handful of lane-parallel selects, and `b` only
-  // its scalar fields (side to move, castling rooks, en passant); each ply's
-  // bitboards are ballots of the lanes, stored to LDS at once (never carried
-  // from ply to ply in registers).  S[0] is the board before the window.
-  uint32_t sqv = R::lane_square(b, lane);
+  // The chain keeps the board as lane bytes — lane l holds square l's piece
+  // (sqv), so a move is a handful of lane-parallel selects — plus the
+  // wave-uniform scalars (side to move, castling rooks, en passant, pockets).
+  // Each ply's board is one byte per lane into SNAP; the checking lanes turn
+  // snapshots back into bitboards.
+  Sc sc = first_lane(R::scalars(root));
+  uint32_t sqv = R::lane_square(root, lane);
+  reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
 
   // ---- windows of up to 64 moves ----
   uint32_t p = m0;   // next text character to tokenise
@@ -237,32 +265,59 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
       break;
     }
     const uint32_t k = min(min(ntok, 64u), nmoves - done);
-    // (b) the chain: interpret and play each move (wave-uniform), boards to LDS
+    // (b) the chain, wave-uniform: interpret and play each move.  Lane j
+    // collects move j's code, the move and the scalars after it,
+    // SNAP[j + 1] the board after it.
+    const uint32_t myc = TK[lane];
+    const Sc sc0 = sc;
+    uint32_t mvw = 0;
+    uint32_t scw[kScw];
+#pragma unroll
+    for (int w = 0; w < kScw; ++w) scw[w] = 0;
     uint32_t kplay = k;
     for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t code = __builtin_amdgcn_readfirstlane(TK[j]);
+      const uint32_t code = lane_value(myc, (int)j);
       Move m;
-      if ((code & kTokBad) || !R::interpret(b, code, m, sqv)) {
+      if ((code & kTokBad) || !R::interpret(sc, code, m, sqv)) {
         kplay = j;
         break;
       }
-      R::play(b, m, sqv, lane);
-      if (lane == 0) {
-        S[j + 1] = b;
-        MV[j] = m;
-      }
+      R::play(sc, m, sqv, lane);
+      reinterpret_cast<uint8_t*>(SNAP[j + 1])[lane] = (uint8_t)sqv;
+      const bool mine = (uint32_t)lane == j;
+      mvw = mine ? R::pack_move(m) : mvw;
+      uint32_t cur[kScw];
+      __builtin_memcpy(cur, &sc, sizeof(Sc));
+#pragma unroll
+      for (int w = 0; w < kScw; ++w) scw[w] = mine ? cur[w] : scw[w];
     }
     lds_fence();
     // (c) lane j checks move j against the board before it and packs the board after it
     bool fail = false;
-    if ((uint32_t)lane < kplay) {
-      const Board before = S[lane];
-      fail = !R::verify(before, TK[lane], MV[lane]);
-      if (!fail) {
-        const Board after = S[lane + 1];
-        const uint32_t o = o0 + done + lane + 1;
-        if (out) out[o] = R::pack(after);
-        if (states) states[o] = after;
+    {
+      uint32_t sb[kScw], s0[kScw];
+      __builtin_memcpy(s0, &sc0, sizeof(Sc));
+#pragma unroll
+      for (int w = 0; w < kScw; ++w) {  // scalars before move j: after move j - 1, or the window's own
+        const uint32_t up = (uint32_t)__shfl_up((int)scw[w], 1, 64);
+        sb[w] = lane == 0 ? s0[w] : up;
+      }
+      if ((uint32_t)lane < kplay) {
+        Sc before_sc, after_sc;
+        __builtin_memcpy(&before_sc, sb, sizeof(Sc));
+        __builtin_memcpy(&after_sc, scw, sizeof(Sc));
+        uint32_t wb[16], wa[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          wb[i] = SNAP[lane][i];
+          wa[i] = SNAP[lane + 1][i];
+        }
+        fail = !R::verify(R::board_from(wb, before_sc), R::unpack_move(mvw));
+        if (!fail) {
+          const uint32_t o = o0 + done + lane + 1;
+          if (out) out[o] = R::pack_from(wa, after_sc);
+          if (states) states[o] = R::board_from(wa, after_sc);
+        }
       }
     }
     const uint64_t fails = __ballot(fail);
@@ -274,11 +329,8 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     }
     done += k;
     ntok -= k;
-    // the next window starts from the board after this one's last move
-    static_assert(sizeof(Board) % 4 == 0 && sizeof(Board) <= 256, "board copy by dwords");
-    if ((uint32_t)lane < sizeof(Board) / 4)
-      reinterpret_cast<uint32_t*>(&S[0])[lane] = reinterpret_cast<const uint32_t*>(&S[k])[lane];
-    // drop the consumed codes
+    // drop the consumed codes; the next window starts from the board after
+    // this one's last move (the lanes' bytes)
     uint32_t keep[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -286,6 +338,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
       keep[r] = src < (uint32_t)kTokRing ? TK[src] : 0;
     }
     lds_fence();
+    reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
 #pragma unroll
     for (int r = 0; r < 2; ++r)
       if ((uint32_t)lane + 64 * r < ntok) TK[lane + 64 * r] = keep[r];
@@ -312,7 +365,10 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   }
   if (final) {
     lds_fence();
-    const Board last = in_vgprs(S[0]);
+    uint32_t wl[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wl[i] = SNAP[0][i];
+    const Board last = in_vgprs(R::board_from(wl, sc));
     const bool any = __ballot(R::any_legal_from(last, lane, lane == 0)) != 0;
     if (lane == 0) final[g] = R::end_flags(last, any);
   }

@@ -84,7 +84,8 @@ FNNUE_HD uint64_t pawn_att(int c, int s) {  // squares a pawn of colour c on s a
 // shifts left; `mask` removes squares that wrapped around a board edge.
 template <int SH>
 FNNUE_HD uint64_t shl(uint64_t b) {
-  return SH > 0 ? b << SH : b >> -SH;
+  if constexpr (SH > 0) return b << SH;
+  else return b >> -SH;
 }
 template <int SH>
 FNNUE_HD uint64_t fill(uint64_t gen, uint64_t empty, uint64_t mask) {

@@ -37,7 +37,42 @@ struct VariantRules {
   using Board = vb::VBoard;
   using Move = vb::VMove;
   using Pos = fnnue_vpos;
-  __device__ static vb::VBoard uniform(const vb::VBoard& b) { return replay::first_lane(b); }
+  // the board's non-square state: pockets, castling rooks (VBoard::cr bytes),
+  // en passant, side to move, variant | c960 << 8
+  struct Scalars {
+    uint64_t pocket[2];
+    uint32_t cr;
+    int32_t ep;
+    uint32_t stm;
+    uint32_t vc;
+  };
+  __device__ static Scalars scalars(const vb::VBoard& b) {
+    Scalars s;
+    s.pocket[0] = b.pocket[0];
+    s.pocket[1] = b.pocket[1];
+    uint32_t cr;
+    __builtin_memcpy(&cr, b.cr, 4);
+    s.cr = cr;
+    s.ep = b.ep;
+    s.stm = b.stm;
+    s.vc = (uint32_t)b.variant | ((uint32_t)b.c960 << 8);
+    return s;
+  }
+  __device__ static int sc_cr(uint32_t cr, int c, int side) {
+    return (int)(int8_t)((cr >> (8 * (2 * c + side))) & 0xFFu);
+  }
+  __device__ static void sc_cr_set(uint32_t& cr, int c, int side, int v) {
+    const int sh = 8 * (2 * c + side);
+    cr = (cr & ~(0xFFu << sh)) | (((uint32_t)v & 0xFFu) << sh);
+  }
+  __device__ static int sc_hand(const Scalars& s, int c, int t) {
+    return (int)(((c ? s.pocket[1] : s.pocket[0]) >> (8 * (t - 1))) & 255u);
+  }
+  __device__ static void sc_hand_add(Scalars& s, int c, int t, int d) {
+    const uint64_t delta = (uint64_t)(int64_t)d << (8 * (t - 1));
+    if (c) s.pocket[1] += delta;
+    else s.pocket[0] += delta;
+  }
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int variant, vb::VBoard& b) {
     return vb::parse_fen(t, p, e, variant, b);
   }
@@ -86,7 +121,7 @@ struct VariantRules {
     }
     return (uint32_t)from | ((uint32_t)to << 6) | ((uint32_t)promo << 12);
   }
-  __device__ static bool interpret(const vb::VBoard& b, uint32_t code, vb::VMove& m, uint32_t sqv) {
+  __device__ static bool interpret(const Scalars& b, uint32_t code, vb::VMove& m, uint32_t sqv) {
     const int to = (int)replay::tok_to(code), pc = (int)replay::tok_piece(code);
     if (code & replay::kTokDrop) {
       m = vb::VMove{-1, (int8_t)to, (int8_t)pc, 2};
@@ -98,10 +133,11 @@ struct VariantRules {
     m = vb::VMove{(int8_t)from, (int8_t)to, (int8_t)pc, 0};
     if ((own & 7u) == (uint32_t)vb::KING && !pc) {
       const int back = b.stm == 0 ? 0 : 56;
+      const bool c960 = (b.vc >> 8) & 1;
 #pragma unroll
       for (int side = 0; side < 2; ++side) {
-        const int rsq = vb::cr_get(b, b.stm, side);
-        if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
+        const int rsq = sc_cr(b.cr, b.stm, side);
+        if (rsq >= 0 && (to == rsq || (!c960 && to == back + (side == 0 ? 6 : 2)))) {
           m = vb::VMove{(int8_t)from, (int8_t)rsq, 0, 1};
           return true;
         }
@@ -109,7 +145,6 @@ struct VariantRules {
     }
     return true;
   }
-  __device__ static void do_move(vb::VBoard& b, const vb::VMove& m) { vb::do_move(b, m); }
   // lane byte: piece code, bit 4 = promoted (crazyhouse)
   __device__ static uint32_t lane_square(const vb::VBoard& b, int sq) {
     return (uint32_t)vb::piece_at(b, sq) | ((uint32_t)((b.promoted >> sq) & 1) << 4);
@@ -117,15 +152,16 @@ struct VariantRules {
   // vb::do_move with lane l holding square l (see ChessRules::play): drops,
   // castling (the rook keeps its promoted mark), captures to the pocket (a
   // promoted piece as a pawn), atomic explosions as one select per lane.
-  __device__ static void play(vb::VBoard& b, const vb::VMove& m, uint32_t& sqv, int lane) {
-    using namespace vb;
+  __device__ static void play(Scalars& b, const vb::VMove& m, uint32_t& sqv, int lane) {
+    using vb::mkpc;
     constexpr int PAWN = vb::PAWN, ROOK = vb::ROOK, KING = vb::KING;
     const int us = b.stm;
+    const int variant = (int)(b.vc & 255u);
     uint32_t v = sqv;
     int new_ep = -1;
     if (m.kind == 2) {
       v = lane == m.to ? (uint32_t)mkpc(us, m.piece) : v;
-      hand_add(b, us, m.piece, -1);
+      sc_hand_add(b, us, m.piece, -1);
     } else if (m.kind == 1) {
       const int back = us == 0 ? 0 : 56;
       const bool king_side = m.to > m.from;
@@ -134,7 +170,8 @@ struct VariantRules {
       v = (lane == m.from || lane == m.to) ? 0u : v;
       v = lane == kto ? (uint32_t)mkpc(us, KING) : v;
       v = lane == rto ? ((uint32_t)mkpc(us, ROOK) | rook_flag) : v;
-      cr_clear(b, us);
+      sc_cr_set(b.cr, us, 0, -1);
+      sc_cr_set(b.cr, us, 1, -1);
     } else {
       const uint32_t moved = replay::lane_value(v, m.from);
       const int pc = (int)(moved & 15u);
@@ -143,43 +180,96 @@ struct VariantRules {
         cap_sq = m.to + (us == 0 ? -8 : 8);
       const uint32_t capv = replay::lane_value(v, cap_sq);
       const int cap = (int)(capv & 15u);
-      const bool zh = b.variant == kCrazyhouse;
+      const bool zh = variant == vb::kCrazyhouse;
       if (cap && zh) {
         const int t = (capv & 16u) ? PAWN : (cap & 7);
-        if (in_hand(b, us, t) < 255) hand_add(b, us, t, 1);
+        if (sc_hand(b, us, t) < 255) sc_hand_add(b, us, t, 1);
       }
       const uint32_t flag = (zh && (m.piece || (moved & 16u))) ? 16u : 0u;
       v = (lane == m.from || (cap && lane == cap_sq)) ? 0u : v;
       v = lane == m.to ? ((uint32_t)(m.piece ? mkpc(us, m.piece) : pc) | flag) : v;
-      if (cap && b.variant == kAtomic) {
+      if (cap && variant == vb::kAtomic) {
         // the capturer explodes with its victim, and every non-pawn around
-        const bool near = (king_att(m.to) >> lane) & 1;
+        const bool near = (vb::king_att(m.to) >> lane) & 1;
         v = (lane == m.to || (near && v != 0 && (v & 7u) != (uint32_t)PAWN)) ? 0u : v;
       }
       if ((pc & 7) == PAWN && (m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
-      if ((pc & 7) == KING) cr_clear(b, us);
-    }
-    sqv = v;
-    const uint32_t t = v & 7u;
-    b.bc[0] = __ballot(v != 0 && (v & 15u) < 8);
-    b.bc[1] = __ballot((v & 15u) >= 8);
-#pragma unroll
-    for (int k = 1; k <= KING; ++k) b.bt[k] = __ballot(t == (uint32_t)k);
-    b.promoted = __ballot((v & 16u) != 0);
-    // castling rights end with the rook (moved, captured, exploded) or the king
-    for (int c = 0; c < 2; ++c) {
-      if (!(b.bt[KING] & colour(b, c))) cr_clear(b, c);
-      for (int side = 0; side < 2; ++side) {
-        const int r = cr_get(b, c, side);
-        if (r >= 0 && (replay::lane_value(v, r) & 15u) != (uint32_t)mkpc(c, ROOK)) cr_set(b, c, side, -1);
+      if ((pc & 7) == KING) {
+        sc_cr_set(b.cr, us, 0, -1);
+        sc_cr_set(b.cr, us, 1, -1);
       }
     }
-    b.ep = (int8_t)new_ep;
-    b.stm = (uint8_t)(us ^ 1);
+    sqv = v;
+    // castling rights end with the rook (moved, captured, exploded) or the king
+    const uint64_t kings = __ballot((v & 7u) == (uint32_t)KING);
+    const uint64_t black = __ballot((v & 15u) >= 8);
+    for (int c = 0; c < 2; ++c) {
+      if (!(kings & (c ? black : ~black))) {
+        sc_cr_set(b.cr, c, 0, -1);
+        sc_cr_set(b.cr, c, 1, -1);
+      }
+      for (int side = 0; side < 2; ++side) {
+        const int r = sc_cr(b.cr, c, side);
+        if (r >= 0 && (replay::lane_value(v, r) & 15u) != (uint32_t)mkpc(c, ROOK)) sc_cr_set(b.cr, c, side, -1);
+      }
+    }
+    b.ep = new_ep;
+    b.stm = (uint32_t)(us ^ 1);
+  }
+  __device__ static uint32_t pack_move(const vb::VMove& m) {
+    uint32_t w;
+    __builtin_memcpy(&w, &m, 4);
+    return w;
+  }
+  __device__ static vb::VMove unpack_move(uint32_t w) {
+    vb::VMove m;
+    __builtin_memcpy(&m, &w, 4);
+    return m;
+  }
+  // A snapshot's bytes as bitboards (bit k of a code = plane k; bit 4 promoted).
+  __device__ static vb::VBoard board_from(const uint32_t (&w)[16], const Scalars& sc) {
+    const uint64_t p0 = replay::byte_plane(w, 0), p1 = replay::byte_plane(w, 1), p2 = replay::byte_plane(w, 2);
+    const uint64_t p3 = replay::byte_plane(w, 3), p4 = replay::byte_plane(w, 4);
+    const uint64_t occ = p0 | p1 | p2;
+    vb::VBoard b;
+    b.bc[0] = occ & ~p3;
+    b.bc[1] = occ & p3;
+    b.bt[0] = 0;
+    b.bt[vb::PAWN] = p0 & ~p1 & ~p2;
+    b.bt[vb::KNIGHT] = ~p0 & p1 & ~p2;
+    b.bt[vb::BISHOP] = p0 & p1 & ~p2;
+    b.bt[vb::ROOK] = ~p0 & ~p1 & p2;
+    b.bt[vb::QUEEN] = p0 & ~p1 & p2;
+    b.bt[vb::KING] = ~p0 & p1 & p2;
+    b.promoted = p4;
+    b.pocket[0] = sc.pocket[0];
+    b.pocket[1] = sc.pocket[1];
+    __builtin_memcpy(b.cr, &sc.cr, 4);
+    b.ep = (int8_t)sc.ep;
+    b.stm = (uint8_t)sc.stm;
+    b.variant = (uint8_t)(sc.vc & 255u);
+    b.c960 = (uint8_t)((sc.vc >> 8) & 255u);
+    return b;
+  }
+  __device__ static fnnue_vpos pack_from(const uint32_t (&w)[16], const Scalars& sc) {
+    uint32_t q[12];
+    uint32_t nib[8];
+    replay::pack_nibbles(w, nib);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = nib[i];
+    // byte 32 stm, bytes 33..42 the pockets (white P N B R Q, black P N B R Q)
+    const uint64_t wp = sc.pocket[0], bp = sc.pocket[1];
+    q[8] = sc.stm | ((uint32_t)(wp & 0xFFFFFFu) << 8);
+    q[9] = (uint32_t)((wp >> 24) & 0xFFFFu) | ((uint32_t)(bp & 0xFFFFu) << 16);
+    q[10] = (uint32_t)((bp >> 16) & 0xFFFFFFu);
+    q[11] = 0;
+    fnnue_vpos p;
+    memcpy(&p, q, sizeof(p));
+    return p;
   }
   // As for chess (builder.hip ChessRules::verify): the token is accepted iff
   // the move interpret() built from it is legal.
-  __device__ static bool verify(const vb::VBoard& b, uint32_t, const vb::VMove& m) {
+  __device__ static bool verify(const vb::VBoard& b, const vb::VMove& m) {
     if (!vb::pseudo_member(b, m)) return false;
     vb::VBoard c = b;
     vb::do_move(c, m);
