@@ -607,6 +607,13 @@ def main():
             for e in ctxs:
                 e.check()
 
+    # FNNUE_STEP_EVENTS=1 (diagnostic runs only, never the driver's): every
+    # step on a stream of torch's own (the evaluator then runs on it, so a
+    # torch event pair brackets each step's GPU work)
+    diag_stream = torch.cuda.Stream() if os.environ.get("FNNUE_STEP_EVENTS") and launch == "single" else None
+    if diag_stream is not None:
+        torch.cuda.set_stream(diag_stream)
+        streams = [diag_stream.cuda_stream]
     for _ in range(args.warmup):
         step()
     sync_all()
@@ -621,13 +628,22 @@ def main():
     if dist_on:
         dist.barrier()
     sync_all()
+    # (per-step GPU times of a short run against a long one: warm-up, clock or box?)
+    step_events = [] if diag_stream is not None else None
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        if step_events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         step()
+        if step_events is not None:
+            ev[1].record()
+            step_events.append(ev)
     sync_all()
     if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = [round(a.elapsed_time(b), 4) for a, b in step_events] if step_events is not None else None
     launches, plan_ms, ft_ms, stack_ms = evs[0][0].timing_phases()
     small_t = evs[1][0].timing_phases() if len(evs) > 1 else None
     if ft_only:
@@ -911,6 +927,8 @@ def main():
             "small_net": small,
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
+        if step_ms is not None:
+            out["step_ms"] = step_ms
         print(json.dumps(out), flush=True)
     for ctxs in evs:
         for e in ctxs:
