@@ -872,6 +872,9 @@ def main():
         "gather_equivalent_GBps": round(bytes_per_launch / (ft_avg * 1e-3) / 1e9, 1) if ft_avg > 0 else None,
         "algorithmic_bytes_per_launch": int(bytes_per_launch),
         "counters": {"source": src, "tree_matches": tree_ok},
+        "live_times": ("overlapped: the big and the small net's kernels share the CUs on two streams (dual call); "
+                       "counters were profiled per net alone, so these fractions are lower bounds of each kernel's "
+                       "own rate (a --no-dual run gives unshared times)") if dual else "kernel alone on the device",
         "note": "frac = the largest of VALU-issue / LDS-busy / HBM fractions of the dominant kernel (counters per "
                 "launch from the committed profile of this tree, over the live kernel time here; peaks at the "
                 "2.4 GHz spec clock); gather_equivalent_GBps = SURVEY §8d algorithmic bytes (every feature row "
@@ -888,7 +891,9 @@ def main():
             sb = max(sfr, key=lambda k: sfr[k]["frac"])
             small["roofline"] = {"kernel": main_k, "bound": sb, "frac": sfr[sb]["frac"], "fractions": sfr,
                                  "counters": {"source": db.get("source"), "tree_matches": tree_ok,
-                                              "key": f"{args.workload}@{args.small_net}"}}
+                                              "key": f"{args.workload}@{args.small_net}"},
+                                 "live_times": "overlapped with the big net's kernels (dual call)" if dual
+                                 else "second call, alone on the device"}
         small["how"] = ("one fnnue_eval_groups_dual_device call per step: one plan, the small net's FT + stacks on "
                         "the small context's stream beside the big net's FT and stacks" if dual else
                         "a second evaluation call per step on the small net's context")

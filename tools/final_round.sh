@@ -56,3 +56,5 @@ b crazyhouse --workload crazyhouse --no-host-api
 b atomic --workload atomic --no-host-api
 b crazyhouse-games --workload crazyhouse-games --no-host-api
 b atomic-games --workload atomic-games --no-host-api
+b games_small_nodual --workload games --small-net 128 --no-dual --no-host-api
+b backend --workload backend
