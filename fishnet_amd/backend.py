@@ -172,14 +172,14 @@ class GpuEvalStub:
 class _Stats(C.Structure):
     _fields_ = [("prep_ms", C.c_double), ("device_ms", C.c_double), ("fill_ms", C.c_double), ("total_ms", C.c_double),
                 ("positions", C.c_uint64), ("stream_syncs", C.c_uint32), ("rebuilds", C.c_uint32),
-                ("host_threads", C.c_uint32), ("reserved", C.c_uint32)]
+                ("host_threads", C.c_uint32), ("pieces", C.c_uint32)]
 
 
 def last_stats(actor: "GpuEvalActor") -> dict:
     """fnnue_backend_last_stats: where the last go() spent its time."""
     st = _Stats()
     N.check(N.lib.fnnue_backend_last_stats(actor._h, C.byref(st)))
-    return {k: getattr(st, k) for k, _ in _Stats._fields_ if k != "reserved"}
+    return {k: getattr(st, k) for k, _ in _Stats._fields_}
 
 
 class _Nets(C.Structure):

@@ -12,15 +12,18 @@
 // there and the plies are evaluated incrementally along each game.
 //
 // One go(), per net: the host counts each batch's plies (it must: the
-// response offsets are part of the answer), stages the text, offsets and the
-// move-work children in one pinned buffer and sends it with one copy; the
-// stream runs the replay (one wave per game), the CHAIN evaluation and the
-// children's evaluation, and one copy brings back the builder's error word,
-// the game-end flags and every (psqt, positional); the host waits once.
-// Buffers are grow-only (device and pinned host), so a steady stream of calls
-// allocates nothing.  A failed batch costs a second pass for its net only.
-// Large calls spread the host work (text staging, response fill) over a few
-// threads.
+// response offsets are part of the answer) and cuts the games into pieces;
+// per piece it stages the text, offsets (and, in the last piece, the
+// move-work children) in a pinned image and sends it with one copy; the
+// net's replay stream runs the replay (one wave per game), the context's
+// stream the CHAIN evaluation and the children's evaluation, and one copy
+// brings back the builder's error word, the game-end flags and every (psqt,
+// positional).  Pieces overlap: the next piece's copy and replay run beside
+// this one's evaluation, and the host writes a piece's responses while the
+// device works on the later ones.  Buffers are grow-only (device and pinned
+// host), so a steady stream of calls allocates nothing.  A failed batch costs
+// a second pass for its piece only.  Large calls spread the host work (text
+// staging, response fill) over a few threads.
 #include "../../include/fnnue_backend.h"
 
 #include <algorithm>
@@ -28,12 +31,14 @@
 #include <chrono>
 #include <climits>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
+#include <emmintrin.h>
 #include <vector>
 
 #include "board.h"
@@ -186,18 +191,39 @@ class Workers {
   bool quit_ = false;
 };
 
-inline unsigned is_ws(unsigned char c) { return (c == ' ') | (c == '\t') | (c == '\n') | (c == '\r'); }
 
-// Whitespace-separated tokens of s[0, n) — the builder's rule (replay_wave.h).
-size_t count_tokens(const char* s, size_t n) {
-  if (!n) return 0;
-  const unsigned char* u = reinterpret_cast<const unsigned char*>(s);
-  size_t c = is_ws(u[0]) ^ 1u;
-  for (size_t i = 1; i < n; ++i) c += (is_ws(u[i]) ^ 1u) & is_ws(u[i - 1]);
-  return c;
+// Whitespace-separated tokens of a NUL-terminated string — the builder's rule
+// (replay_wave.h: blanks are ' ', '\t', '\n', '\r'; a token starts at a
+// non-blank byte whose predecessor is blank or the string's start) — in one
+// pass, 16 bytes at a time (aligned loads: never past the page holding the
+// terminator); *len = the string's length.
+size_t scan_tokens(const char* s, size_t* len) {
+  const char* base = reinterpret_cast<const char*>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
+  const __m128i sp = _mm_set1_epi8(' '), tab = _mm_set1_epi8('\t'), nl = _mm_set1_epi8('\n'), cr = _mm_set1_epi8('\r');
+  uint32_t pre = (1u << (s - base)) - 1;  // bytes before s: blank, not the end
+  uint32_t prev_ws = 1;
+  size_t tokens = 0;
+  for (const char* p = base;; p += 16, pre = 0) {
+    const __m128i v = _mm_load_si128(reinterpret_cast<const __m128i*>(p));
+    uint32_t z = (uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_setzero_si128())) & ~pre;
+    const __m128i w = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, sp), _mm_cmpeq_epi8(v, tab)),
+                                   _mm_or_si128(_mm_cmpeq_epi8(v, nl), _mm_cmpeq_epi8(v, cr)));
+    uint32_t ws = (uint32_t)_mm_movemask_epi8(w) | pre;
+    if (z) ws |= ~((1u << __builtin_ctz(z)) - 1) & 0xFFFFu;  // the terminator and what follows: blank
+    const uint32_t starts = ~ws & ((ws << 1) | prev_ws) & 0xFFFFu;
+    tokens += (size_t)__builtin_popcount(starts);
+    if (z) {
+      *len = (size_t)(p - s) + (size_t)__builtin_ctz(z);
+      return tokens;
+    }
+    prev_ws = (ws >> 15) & 1u;
+  }
 }
 
-size_t count_moves(const char* s) { return s ? count_tokens(s, std::strlen(s)) : 0; }
+size_t count_moves(const char* s) {
+  size_t len = 0;
+  return s ? scan_tokens(s, &len) : 0;
+}
 
 int64_t to_cp(int32_t psqt, int32_t positional, int32_t norm) {
   const int64_t v = ((int64_t)psqt + positional) / 16;  // OutputScale, C truncation
@@ -300,11 +326,27 @@ int variant_move_root(int variant, const fnnue_acquired& a, MoveRoot& R, std::ve
   return FNNUE_OK;
 }
 
-// One net's share of a go(): its analysis games and its move-work roots,
-// staged in one pinned host image and one device image of the same layout
-//   [text | fen_off | mv_off | ply_off | children | err | fin | psqt | positional]
-// the first five parts (and the zeroed error word) go up with one copy, the
-// last four come back with one.
+// One piece of a net's work: a run of its analysis games (the net's last piece
+// also carries the move-work children), staged as one image
+//   [text | fen_off | mv_off | ply_off | children | err (16 B) | fin | psqt | positional]
+// at its own place in the net's buffers: the first five parts and the zeroed
+// error word go up with one copy, the last four come back with one.
+struct Piece {
+  std::vector<size_t> games;  // analysis batches (job indices)
+  bool kids = false;          // the net's move-work children ride in this piece
+  uint32_t ng = 0, n = 0;     // games, plies
+  size_t nk = 0;              // children
+  size_t o_fen = 0, o_mv = 0, o_ply = 0, o_kids = 0, o_res = 0, o_fin = 0, o_ps = 0, o_po = 0, end = 0;
+  size_t up0 = 0, down0 = 0, dev0 = 0, pos0 = 0;  // where the piece lives in the net's buffers
+  bool pending = false;                           // evaluation enqueued, results not yet read
+};
+
+// One net's share of a go(): its analysis games cut into pieces of about
+// piece_plies plies, and its move-work roots.  A piece's upload and replay run
+// on the net's replay stream, its evaluation and download on the context's
+// stream (after the replay's event): the next piece's upload and replay
+// overlap this piece's evaluation, and the host writes a piece's responses
+// while the device works on the later ones.
 struct NetWork {
   std::vector<size_t> games;      // analysis batches (job indices)
   std::vector<size_t> roots;      // move batches whose roots have legal children
@@ -313,11 +355,11 @@ struct NetWork {
   std::vector<uint8_t> kids;      // children records
   std::vector<size_t> terminal;   // move batches whose root has no legal move
   std::vector<MoveRoot> troots;
-  std::vector<uint32_t> toff;     // text offset of each game in the image
+  std::vector<Piece> pieces;
   size_t nk = 0, rec = 0;
-  size_t o_fen = 0, o_mv = 0, o_ply = 0, o_kids = 0, o_res = 0, o_fin = 0, o_ps = 0, o_po = 0, end = 0;
-  uint32_t ng = 0, n = 0;
-  bool pending = false;
+  size_t next = 0;                // first piece whose responses are not written yet
+  hipStream_t rs = nullptr;       // replay stream
+  std::vector<hipEvent_t> ev_up, ev_done;  // per piece: replayed; results and error word on the host
   DevBuf dev, pos;
   PinnedBuf up, down, cerr;
   void clear() {
@@ -328,9 +370,22 @@ struct NetWork {
     kids.clear();
     terminal.clear();
     troots.clear();
+    pieces.clear();
     nk = 0;
-    ng = n = 0;
-    pending = false;
+    next = 0;
+  }
+  int events(size_t n) {
+    while (ev_up.size() < n) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) return fail(FNNUE_E_DEVICE, "hipEventCreate");
+      if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        return fail(FNNUE_E_DEVICE, "hipEventCreate");
+      }
+      ev_up.push_back(a);
+      ev_done.push_back(b);
+    }
+    return FNNUE_OK;
   }
   void release() {
     dev.release();
@@ -338,8 +393,16 @@ struct NetWork {
     up.release();
     down.release();
     cerr.release();
+    for (hipEvent_t e : ev_up) (void)hipEventDestroy(e);
+    for (hipEvent_t e : ev_done) (void)hipEventDestroy(e);
+    ev_up.clear();
+    ev_done.clear();
+    if (rs) (void)hipStreamDestroy(rs);
+    rs = nullptr;
   }
 };
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
@@ -347,6 +410,9 @@ struct fnnue_backend {
   fnnue_ctx* ctx[kKinds] = {};  // one evaluator per net, all on one device
   int device = 0;
   int32_t norm = kNormalizeToPawnSf151;
+  size_t piece_plies = 262144;  // FNNUE_BACKEND_PIECE_PLIES
+  int replay_cus = 0;           // FNNUE_BACKEND_REPLAY_CUS: > 0 = the replay stream on that many CUs
+  bool replay_serial = false;   // FNNUE_BACKEND_REPLAY_SERIAL: replay on the evaluation stream
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;  // slot / done / stop changes
@@ -356,15 +422,37 @@ struct fnnue_backend {
   int pool_threads = 1;
   NetWork net[kKinds];
   std::vector<uint32_t> flen, mlen;  // per batch of the job in flight: FEN / moves text lengths
-  std::vector<uint8_t> skip;         // per response: skipPositions
+  std::vector<int8_t> kind;          // per batch: its net slot
+  std::vector<uint8_t> bskip;        // per batch: has skipPositions
+  std::vector<uint8_t> skip;         // per response of such a batch: skipped
   std::mutex stats_mu;
   fnnue_backend_stats stats{};
+  // per go(): its clock, positions written so far, host time spent writing / waiting
+  Clock::time_point t0;
+  uint64_t filled = 0;
+  double fill_ms = 0, wait_ms = 0;
+  uint32_t syncs = 0, rebuilds = 0;
+  // FNNUE_BACKEND_TRACE=1: each go() prints its host timeline (µs since the
+  // call started) to stderr — diagnostics only
+  bool trace = false;
+  std::string tl;
+  void mark(const char* what, int k = -1, long pi = -1) {
+    if (!trace) return;
+    char b[96];
+    std::snprintf(b, sizeof(b), "%s[\"%s\",%d,%ld,%.1f]", tl.empty() ? "" : ",", what, k, pi, ms_since(t0) * 1e3);
+    tl += b;
+  }
 
   void run(Job& j);
   int prepare_moves(Job& j, int k);
-  int stage(Job& j, int k);
-  int collect(Job& j, int k, uint32_t* syncs, uint32_t* rebuilds);
-  void fill(Job& j, int k, uint64_t ms, uint32_t nps);
+  void layout(const Job& j, int k, Piece& P);
+  int plan(Job& j, int k);
+  int stage_up(Job& j, int k, size_t pi);
+  int stage_eval(int k, size_t pi);
+  int finish(Job& j, int k, bool wait, bool* ready);
+  int recover(Job& j, int k, size_t pi);
+  void fill(Job& j, int k, const Piece& P);
+  void fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint32_t nps);
   void loop() {
     std::unique_lock<std::mutex> lk(mu);
     for (;;) {
@@ -427,130 +515,245 @@ int fnnue_backend::prepare_moves(Job& j, int k) {
   return FNNUE_OK;
 }
 
-// Host image of one net's work, then its device work on the net's stream:
-// H2D, replay, CHAIN evaluation, children evaluation, D2H.  Nothing waits.
-int fnnue_backend::stage(Job& j, int k) {
-  NetWork& W = net[k];
-  fnnue_ctx* c = ctx[k];
-  hipStream_t s = c->stream;
-  const bool chess = k == kVariantChess;
-  W.ng = (uint32_t)W.games.size();
+// A piece's image layout from its games (offsets relative to the piece).
+void fnnue_backend::layout(const Job& j, int k, Piece& P) {
+  const NetWork& W = net[k];
   size_t text = 0, plies = 0;
-  W.toff.resize(W.ng);
-  for (uint32_t g = 0; g < W.ng; ++g) {
-    const size_t i = W.games[g];
-    W.toff[g] = (uint32_t)text;
+  for (size_t i : P.games) {
     text += flen[i] + 1 + mlen[i];
     plies += j.off[i + 1] - j.off[i];
   }
-  if (text >= (1ull << 31) || plies >= (1ull << 31)) return fail(FNNUE_E_ARG, "batch text too large");
-  W.n = (uint32_t)plies;
-  const size_t ng = W.ng, n = W.n, nk = W.nk;
-  W.o_fen = align16(text);
-  W.o_mv = W.o_fen + 4 * (ng + 1);
-  W.o_ply = W.o_mv + 4 * ng;
-  W.o_kids = align16(W.o_ply + 4 * (ng + 1));
-  W.o_res = align16(W.o_kids + nk * W.rec);
-  W.o_fin = W.o_res + 16;
-  W.o_ps = align16(W.o_fin + ng);
-  W.o_po = W.o_ps + 4 * (n + nk);
-  W.end = W.o_po + 4 * (n + nk);
-  if (int rc = W.dev.reserve(W.end)) return rc;
-  if (int rc = W.up.reserve(W.o_res + 16)) return rc;
-  if (int rc = W.down.reserve(W.end - W.o_res)) return rc;
-  if (int rc = W.cerr.reserve(4)) return rc;
-  if (ng)
-    if (int rc = W.pos.reserve(n * W.rec)) return rc;
-  char* img = W.up.at<char>(0);
-  uint32_t* fo = W.up.at<uint32_t>(W.o_fen);
-  uint32_t* mo = W.up.at<uint32_t>(W.o_mv);
-  uint32_t* po = W.up.at<uint32_t>(W.o_ply);
-  uint32_t acc = 0;
-  for (uint32_t g = 0; g < W.ng; ++g) {
-    const size_t i = W.games[g];
-    fo[g] = W.toff[g];
-    mo[g] = W.toff[g] + flen[i];
+  P.ng = (uint32_t)P.games.size();
+  P.n = (uint32_t)plies;
+  P.nk = P.kids ? W.nk : 0;
+  const size_t ng = P.ng, n = P.n, nk = P.nk;
+  P.o_fen = align16(text);
+  P.o_mv = P.o_fen + 4 * (ng + 1);
+  P.o_ply = P.o_mv + 4 * ng;
+  P.o_kids = align16(P.o_ply + 4 * (ng + 1));
+  P.o_res = align16(P.o_kids + nk * W.rec);
+  P.o_fin = P.o_res + 16;
+  P.o_ps = align16(P.o_fin + ng);
+  P.o_po = P.o_ps + 4 * (n + nk);
+  P.end = P.o_po + 4 * (n + nk);
+}
+
+// Cuts the net's games into pieces and places them in its (grow-only) buffers.
+int fnnue_backend::plan(Job& j, int k) {
+  NetWork& W = net[k];
+  W.pieces.clear();
+  size_t acc = 0, plies = 0;
+  for (size_t i : W.games) {
+    if (W.pieces.empty() || acc >= piece_plies) {
+      W.pieces.emplace_back();
+      acc = 0;
+    }
+    W.pieces.back().games.push_back(i);
+    acc += j.off[i + 1] - j.off[i];
+    plies += j.off[i + 1] - j.off[i];
+  }
+  if (plies >= (1ull << 31)) return fail(FNNUE_E_ARG, "batch too large");
+  if (W.nk) {
+    if (W.pieces.empty()) W.pieces.emplace_back();
+    W.pieces.back().kids = true;
+  }
+  size_t up = 0, down = 0, dev = 0, pos = 0;
+  for (Piece& P : W.pieces) {
+    layout(j, k, P);
+    if (P.o_fen >= (1ull << 31)) return fail(FNNUE_E_ARG, "batch text too large");
+    P.up0 = up;
+    P.down0 = down;
+    P.dev0 = dev;
+    P.pos0 = pos;
+    up = align256(up + P.o_res + 16);
+    down = align256(down + P.end - P.o_res);
+    dev = align256(dev + P.end);
+    pos = align256(pos + (size_t)P.n * W.rec);
+  }
+  if (int rc = W.dev.reserve(dev)) return rc;
+  if (int rc = W.up.reserve(up)) return rc;
+  if (int rc = W.down.reserve(down)) return rc;
+  if (int rc = W.cerr.reserve(4 * W.pieces.size())) return rc;
+  if (pos)
+    if (int rc = W.pos.reserve(pos)) return rc;
+  if (!W.rs) {
+    if (replay_serial) {
+      W.rs = nullptr;
+    } else if (replay_cus > 0) {
+      // the replay's waves on replay_cus CUs spread over the device (the
+      // evaluation keeps the others): one mask bit per CU
+      int ncu = 0;
+      HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
+      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+      const int use = std::min(replay_cus, ncu);
+      for (int i = 0; i < use; ++i) {
+        const int cu = (int)((int64_t)i * ncu / use);
+        mask[(size_t)cu / 32] |= 1u << (cu % 32);
+      }
+      HIP_TRY(hipExtStreamCreateWithCUMask(&W.rs, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+    } else {
+      HIP_TRY(hipStreamCreateWithFlags(&W.rs, hipStreamNonBlocking), "hipStreamCreate(replay)");
+    }
+  }
+  return W.events(W.pieces.size());
+}
+
+// Host image of a piece, then on the replay stream: its upload and the
+// replay of its games.  Nothing waits.
+int fnnue_backend::stage_up(Job& j, int k, size_t pi) {
+  NetWork& W = net[k];
+  Piece& P = W.pieces[pi];
+  char* img = W.up.at<char>(P.up0);
+  uint32_t* fo = reinterpret_cast<uint32_t*>(img + P.o_fen);
+  uint32_t* mo = reinterpret_cast<uint32_t*>(img + P.o_mv);
+  uint32_t* po = reinterpret_cast<uint32_t*>(img + P.o_ply);
+  uint32_t text = 0, acc = 0;
+  for (uint32_t g = 0; g < P.ng; ++g) {
+    const size_t i = P.games[g];
+    fo[g] = text;
+    mo[g] = text + flen[i];
     po[g] = acc;
+    text += flen[i] + 1 + mlen[i];
     acc += j.off[i + 1] - j.off[i];
   }
-  fo[ng] = (uint32_t)text;
-  po[ng] = acc;
-  pool.run(ng, 512, [&](size_t lo, size_t hi) {
+  fo[P.ng] = text;
+  po[P.ng] = acc;
+  pool.run(P.ng, 512, [&](size_t lo, size_t hi) {
     for (size_t g = lo; g < hi; ++g) {
-      const fnnue_acquired& a = j.batches[W.games[g]];
-      char* d = img + W.toff[g];
-      const uint32_t fl = flen[W.games[g]], ml = mlen[W.games[g]];
+      const size_t i = P.games[g];
+      const fnnue_acquired& a = j.batches[i];
+      char* d = img + fo[g];
+      const uint32_t fl = flen[i], ml = mlen[i];
       if (fl) std::memcpy(d, a.position, fl);
       d[fl] = ' ';
       if (ml) std::memcpy(d + fl + 1, a.moves, ml);
     }
   });
-  if (nk) std::memcpy(img + W.o_kids, W.kids.data(), nk * W.rec);
-  std::memset(img + W.o_res, 0, 16);
-  HIP_TRY(hipMemcpyAsync(W.dev.p, W.up.p, W.o_res + 16, hipMemcpyHostToDevice, s), "H2D(batch image)");
-  uint32_t* d_err = W.dev.at<uint32_t>(W.o_res);
-  int32_t* d_ps = W.dev.at<int32_t>(W.o_ps);
-  int32_t* d_po = W.dev.at<int32_t>(W.o_po);
-  if (ng) {
-    HIP_TRY(replay_games_device(k, W.dev.at<char>(0), W.dev.at<uint32_t>(W.o_fen), W.dev.at<uint32_t>(W.o_mv),
-                                W.dev.at<uint32_t>(W.o_ply), W.ng, W.pos.p, W.dev.at<uint8_t>(W.o_fin), d_err, s),
+  if (P.nk) std::memcpy(img + P.o_kids, W.kids.data(), P.nk * W.rec);
+  std::memset(img + P.o_res, 0, 16);
+  char* dimg = W.dev.at<char>(P.dev0);
+  hipStream_t us = W.rs ? W.rs : ctx[k]->stream;
+  HIP_TRY(hipMemcpyAsync(dimg, img, P.o_res + 16, hipMemcpyHostToDevice, us), "H2D(batch image)");
+  if (P.ng)
+    HIP_TRY(replay_games_device(k, dimg, reinterpret_cast<uint32_t*>(dimg + P.o_fen),
+                                reinterpret_cast<uint32_t*>(dimg + P.o_mv), reinterpret_cast<uint32_t*>(dimg + P.o_ply),
+                                P.ng, W.pos.at<char>(P.pos0), reinterpret_cast<uint8_t*>(dimg + P.o_fin),
+                                reinterpret_cast<uint32_t*>(dimg + P.o_res), us),
             "batch replay launch");
-    const uint32_t* d_off = W.dev.at<uint32_t>(W.o_ply);
-    const int rc = chess ? fnnue_eval_groups_device(c, static_cast<const fnnue_pos*>(W.pos.p), d_off, ng, n,
-                                                    FNNUE_GROUP_CHAIN, d_ps, d_po, s)
-                         : fnnue_eval_vgroups_device(c, static_cast<const fnnue_vpos*>(W.pos.p), d_off, ng, n,
-                                                     FNNUE_GROUP_CHAIN, d_ps, d_po, s);
-    if (rc) return rc;
-  }
-  if (nk) {
-    const void* d_kids = W.dev.at<char>(W.o_kids);
-    const int rc = chess ? fnnue_eval_positions_device(c, static_cast<const fnnue_pos*>(d_kids), nk, d_ps + n, d_po + n, s)
-                         : fnnue_eval_vpositions_device(c, static_cast<const fnnue_vpos*>(d_kids), nk, d_ps + n,
-                                                        d_po + n, s);
-    if (rc) return rc;
-  }
-  HIP_TRY(hipMemcpyAsync(W.down.p, W.dev.at<char>(W.o_res), W.end - W.o_res, hipMemcpyDeviceToHost, s),
-          "D2H(results)");
-  HIP_TRY(hipMemcpyAsync(W.cerr.p, c->err, 4, hipMemcpyDeviceToHost, s), "D2H(error word)");
-  W.pending = true;
+  HIP_TRY(hipEventRecord(W.ev_up[pi], us), "hipEventRecord(replayed)");
+  mark("up", k, (long)pi);
   return FNNUE_OK;
 }
 
-// Waits for one net's work.  A game the builder rejected (FEN / move) or
-// whose positions the evaluator rejects fails its own batch: it is dropped
-// and the net's work staged again.
-int fnnue_backend::collect(Job& j, int k, uint32_t* syncs, uint32_t* rebuilds) {
+// On the context's stream, after the piece's replay: the CHAIN evaluation of
+// its plies, the children's evaluation, the results and the evaluator's error
+// word to the host.  Nothing waits.
+int fnnue_backend::stage_eval(int k, size_t pi) {
+  NetWork& W = net[k];
+  Piece& P = W.pieces[pi];
+  fnnue_ctx* c = ctx[k];
+  hipStream_t s = c->stream;
+  const bool chess = k == kVariantChess;
+  char* dimg = W.dev.at<char>(P.dev0);
+  int32_t* d_ps = reinterpret_cast<int32_t*>(dimg + P.o_ps);
+  int32_t* d_po = reinterpret_cast<int32_t*>(dimg + P.o_po);
+  HIP_TRY(hipStreamWaitEvent(s, W.ev_up[pi], 0), "hipStreamWaitEvent(replayed)");
+  if (P.ng) {
+    const uint32_t* d_off = reinterpret_cast<const uint32_t*>(dimg + P.o_ply);
+    const void* d_pos = W.pos.at<char>(P.pos0);
+    const int rc = chess ? fnnue_eval_groups_device(c, static_cast<const fnnue_pos*>(d_pos), d_off, P.ng, P.n,
+                                                    FNNUE_GROUP_CHAIN, d_ps, d_po, s)
+                         : fnnue_eval_vgroups_device(c, static_cast<const fnnue_vpos*>(d_pos), d_off, P.ng, P.n,
+                                                     FNNUE_GROUP_CHAIN, d_ps, d_po, s);
+    if (rc) return rc;
+  }
+  if (P.nk) {
+    const void* d_kids = dimg + P.o_kids;
+    const int rc = chess ? fnnue_eval_positions_device(c, static_cast<const fnnue_pos*>(d_kids), P.nk, d_ps + P.n,
+                                                       d_po + P.n, s)
+                         : fnnue_eval_vpositions_device(c, static_cast<const fnnue_vpos*>(d_kids), P.nk, d_ps + P.n,
+                                                        d_po + P.n, s);
+    if (rc) return rc;
+  }
+  HIP_TRY(hipMemcpyAsync(W.down.at<char>(P.down0), dimg + P.o_res, P.end - P.o_res, hipMemcpyDeviceToHost, s),
+          "D2H(results)");
+  HIP_TRY(hipMemcpyAsync(W.cerr.at<uint32_t>(4 * pi), c->err, 4, hipMemcpyDeviceToHost, s), "D2H(error word)");
+  HIP_TRY(hipEventRecord(W.ev_done[pi], s), "hipEventRecord(results)");
+  P.pending = true;
+  mark("eval", k, (long)pi);
+  return FNNUE_OK;
+}
+
+// The net's next piece: when its results are on the host (waiting for them if
+// `wait`), writes its responses — after recovering, if the builder or the
+// evaluator reported an error.  *ready = false: not there yet.
+int fnnue_backend::finish(Job& j, int k, bool wait, bool* ready) {
+  NetWork& W = net[k];
+  const size_t pi = W.next;
+  *ready = false;
+  if (wait) {
+    const auto tw = Clock::now();
+    mark("wait", k, (long)pi);
+    HIP_TRY(hipEventSynchronize(W.ev_done[pi]), "hipEventSynchronize");
+    wait_ms += ms_since(tw);
+    ++syncs;
+  } else {
+    const hipError_t q = hipEventQuery(W.ev_done[pi]);
+    if (q == hipErrorNotReady) return FNNUE_OK;
+    HIP_TRY(q, "hipEventQuery");
+  }
+  *ready = true;
+  Piece& P = W.pieces[pi];
+  P.pending = false;
+  if (W.down.at<uint32_t>(P.down0)[0] || *W.cerr.at<uint32_t>(4 * pi))
+    if (int rc = recover(j, k, pi)) return rc;
+  fill(j, k, P);
+  ++W.next;
+  return FNNUE_OK;
+}
+
+// A game the builder rejected (FEN / move), or whose positions the evaluator
+// rejects, fails its own batch: it is dropped from its piece and the piece is
+// staged again.  The evaluator's error word is sticky and shared by the net's
+// pieces, so the pieces already enqueued behind this one are staged again
+// after it is cleared.
+int fnnue_backend::recover(Job& j, int k, size_t pi) {
   NetWork& W = net[k];
   fnnue_ctx* c = ctx[k];
   hipStream_t s = c->stream;
+  Piece& P = W.pieces[pi];
+  if (W.rs) HIP_TRY(hipStreamSynchronize(W.rs), "hipStreamSynchronize(replay)");
+  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
+  syncs += 2;
+  // The drain also ran the evaluations enqueued behind this piece: whatever
+  // they latched is cleared here, and they are staged again below.
+  HIP_TRY(hipMemsetAsync(c->err, 0, 4, s), "hipMemsetAsync(error word)");
+  bool rebuilt = false;  // the error word was cleared before this piece's own first pass
   for (;;) {
-    HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-    ++*syncs;
-    W.pending = false;
-    const uint32_t* berr = W.down.at<uint32_t>(0);
-    const uint32_t cerr = *W.cerr.at<uint32_t>(0);
-    if (!berr[0] && !cerr) return FNNUE_OK;
-    if (cerr) HIP_TRY(hipMemsetAsync(c->err, 0, 4, s), "hipMemsetAsync(error word)");
+    const uint32_t* berr = W.down.at<uint32_t>(P.down0);
+    const uint32_t cerr = *W.cerr.at<uint32_t>(4 * pi);
+    if (!berr[0] && !cerr) break;
+    if (cerr && rebuilt) HIP_TRY(hipMemsetAsync(c->err, 0, 4, s), "hipMemsetAsync(error word)");
     if (berr[0]) {
       // The builder names the failing game; that batch fails (PositionFailed)
       // and the rest are staged again.  A count mismatch or a game index
-      // outside the batch cannot be blamed on any batch: the call fails.
-      if (berr[0] == kBuildErrCount || berr[1] >= W.ng)
+      // outside the piece cannot be blamed on any batch: the call fails.
+      if (berr[0] == kBuildErrCount || berr[1] >= P.ng)
         return fail(FNNUE_E_DEVICE, "batch builder reported game " + std::to_string(berr[1]) + " of " +
-                                        std::to_string(W.ng) + " (code " + std::to_string(berr[0]) + ")");
-      j.rc[W.games[berr[1]]] = berr[0] == kBuildErrFen ? FNNUE_E_FEN : FNNUE_E_MOVE;
-      W.games.erase(W.games.begin() + berr[1]);
+                                        std::to_string(P.ng) + " (code " + std::to_string(berr[0]) + ")");
+      j.rc[P.games[berr[1]]] = berr[0] == kBuildErrFen ? FNNUE_E_FEN : FNNUE_E_MOVE;
+      P.games.erase(P.games.begin() + berr[1]);
     } else {
       // A FEN the builder parses but the evaluator cannot (kings, > 32
       // pieces): find the games holding such positions, fail those batches.
       // (Move-work children were checked on the host.)
-      std::vector<uint8_t> hpos((size_t)W.n * W.rec);
+      std::vector<uint8_t> hpos((size_t)P.n * W.rec);
       if (!hpos.empty())
-        HIP_TRY(hipMemcpy(hpos.data(), W.pos.p, hpos.size(), hipMemcpyDeviceToHost), "D2H(positions)");
-      ++*syncs;
-      const uint32_t* ply = W.up.at<uint32_t>(W.o_ply);
+        HIP_TRY(hipMemcpy(hpos.data(), W.pos.at<char>(P.pos0), hpos.size(), hipMemcpyDeviceToHost), "D2H(positions)");
+      ++syncs;
+      const uint32_t* ply = W.up.at<uint32_t>(P.up0 + P.o_ply);
       std::vector<size_t> keep;
-      for (uint32_t g = 0; g < W.ng; ++g) {
+      for (uint32_t g = 0; g < P.ng; ++g) {
         bool ok = true;
         for (uint32_t x = ply[g]; x < ply[g + 1] && ok; ++x) {
           const uint8_t* p = hpos.data() + (size_t)x * W.rec;
@@ -558,41 +761,67 @@ int fnnue_backend::collect(Job& j, int k, uint32_t* syncs, uint32_t* rebuilds) {
                                   : host_vpos_state(*reinterpret_cast<const fnnue_vpos*>(p), k) != 0;
         }
         if (ok)
-          keep.push_back(W.games[g]);
+          keep.push_back(P.games[g]);
         else
-          j.rc[W.games[g]] = FNNUE_E_POSITION;
+          j.rc[P.games[g]] = FNNUE_E_POSITION;
       }
-      if (keep.size() == W.games.size())
-        return fail(FNNUE_E_POSITION, "the evaluator rejected a position no batch holds");
-      W.games.swap(keep);
+      if (keep.size() == P.games.size())
+        return fail(cerr & 2u ? FNNUE_E_DEVICE : FNNUE_E_POSITION,
+                    "the evaluator latched error " + std::to_string(cerr) + " on piece " + std::to_string(pi) + " of " +
+                        std::to_string(W.pieces.size()) + " (net " + std::to_string(k) + ", " + std::to_string(P.ng) +
+                        " games, " + std::to_string(P.n) + " plies, pass " + std::to_string(rebuilds) +
+                        ") and no batch of the piece holds an invalid position");
+      P.games.swap(keep);
     }
-    ++*rebuilds;
-    if (int rc = stage(j, k)) return rc;
+    ++rebuilds;
+    rebuilt = true;
+    layout(j, k, P);  // fewer games: the piece still fits its place
+    if (int rc = stage_up(j, k, pi)) return rc;
+    if (int rc = stage_eval(k, pi)) return rc;
+    HIP_TRY(hipEventSynchronize(W.ev_done[pi]), "hipEventSynchronize");
+    ++syncs;
+    P.pending = false;
   }
+  for (size_t q = pi + 1; q < W.pieces.size(); ++q)
+    if (W.pieces[q].pending) {
+      if (int rc = stage_up(j, k, q)) return rc;
+      if (int rc = stage_eval(k, q)) return rc;
+    }
+  return FNNUE_OK;
 }
 
-// Responses of one net's batches from the results image (several threads for
-// large calls): analysis plies as Score::Cp, a game's last ply with no legal
-// move as mate 0 / cp 0; move work as a one-ply search over the children.
-void fnnue_backend::fill(Job& j, int k, uint64_t ms, uint32_t nps) {
+// Responses of one piece's games from its results image (several threads for
+// large pieces): analysis plies as Score::Cp, a game's last ply with no legal
+// move as mate 0 / cp 0; then the move work it carries.  time / nps: the wall
+// time of the go() call until these results were on the host, and the
+// positions evaluated by then per second.
+void fnnue_backend::fill(Job& j, int k, const Piece& P) {
+  const auto tf = Clock::now();
   NetWork& W = net[k];
-  const uint8_t* fin = W.down.at<uint8_t>(W.o_fin - W.o_res);
-  const int32_t* ps = W.down.at<int32_t>(W.o_ps - W.o_res);
-  const int32_t* po = W.down.at<int32_t>(W.o_po - W.o_res);
-  const uint32_t* ply = W.up.at<uint32_t>(W.o_ply);
+  mark("fill", k, (long)(&P - W.pieces.data()));
+  const char* res = W.down.at<char>(P.down0) - P.o_res;  // the results image, at the piece's offsets
+  const uint8_t* fin = reinterpret_cast<const uint8_t*>(res + P.o_fin);
+  const int32_t* ps = reinterpret_cast<const int32_t*>(res + P.o_ps);
+  const int32_t* po = reinterpret_cast<const int32_t*>(res + P.o_po);
+  const uint32_t* ply = W.up.at<uint32_t>(P.up0 + P.o_ply);
+  filled += P.n + P.nk;
+  const double el = ms_since(t0);
+  const uint64_t ms = (uint64_t)el;
+  const uint32_t nps = el > 0 ? (uint32_t)std::min(4.0e9, (double)filled / (el * 1e-3)) : 0;
   const int32_t nrm = norm;
-  pool.run(W.ng, 64, [&](size_t lo, size_t hi) {
+  pool.run(P.ng, 64, [&](size_t lo, size_t hi) {
     for (size_t g = lo; g < hi; ++g) {
-      const size_t i = W.games[g];
+      const size_t i = P.games[g];
       const uint32_t b = j.off[i], len = j.off[i + 1] - b;
       const uint8_t matrix = j.batches[i].multipv > 0 ? 1 : 0;  // Work::matrix_wanted: multipv is Some
+      const bool sk = bskip[i];
       for (uint32_t q = 0; q < len; ++q) {
         fnnue_position_response r;
         std::memset(&r, 0, sizeof(r));
         r.position_id = q;
         r.time_ms = ms;
         r.nps = nps;
-        if (skip[b + q]) {
+        if (sk && skip[b + q]) {
           r.skipped = 1;
         } else {
           const size_t x = ply[g] + q;
@@ -610,19 +839,23 @@ void fnnue_backend::fill(Job& j, int k, uint64_t ms, uint32_t nps) {
       }
     }
   });
-  auto root_response = [&](size_t i) -> fnnue_position_response& {
-    fnnue_position_response& r = j.out[j.off[i]];
+  if (P.kids) fill_roots(j, k, P, ms, nps);
+  fill_ms += ms_since(tf);
+  mark("filled", k, (long)(&P - W.pieces.data()));
+}
+
+// Move work: a one-ply search over each root's children.
+void fnnue_backend::fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint32_t nps) {
+  NetWork& W = net[k];
+  const char* res = W.down.at<char>(P.down0) - P.o_res;
+  const int32_t* kps = reinterpret_cast<const int32_t*>(res + P.o_ps) + P.n;
+  const int32_t* kpo = reinterpret_cast<const int32_t*>(res + P.o_po) + P.n;
+  for (size_t t = 0; t < W.roots.size(); ++t) {
+    const MoveRoot& R = W.mroots[t];
+    fnnue_position_response& r = j.out[j.off[W.roots[t]]];
     std::memset(&r, 0, sizeof(r));
     r.time_ms = ms;
     r.nps = nps;
-    return r;
-  };
-  for (size_t t = 0; t < W.terminal.size(); ++t) terminal_response(root_response(W.terminal[t]), W.troots[t].fin);
-  const int32_t* kps = ps + W.n;
-  const int32_t* kpo = po + W.n;
-  for (size_t t = 0; t < W.roots.size(); ++t) {
-    const MoveRoot& R = W.mroots[t];
-    fnnue_position_response& r = root_response(W.roots[t]);
     // rank: 2 = mates, 1 = evaluated, 0 = never (value orders within a rank)
     size_t best = 0;
     int best_rank = -1;
@@ -656,33 +889,56 @@ void fnnue_backend::fill(Job& j, int k, uint64_t ms, uint32_t nps) {
       r.score = 1;
     } else {
       r.score_kind = FNNUE_SCORE_CP;
-      r.score = bv * 100 / nrm;
+      r.score = bv * 100 / norm;
     }
     std::strncpy(r.best_move, R.uci[best].c_str(), sizeof(r.best_move) - 1);
   }
 }
 
 void fnnue_backend::run(Job& j) {
-  const auto t0 = Clock::now();
+  t0 = Clock::now();
+  tl.clear();
+  filled = 0;
+  fill_ms = wait_ms = 0;
+  syncs = rebuilds = 0;
   const size_t nb = j.nb;
   flen.resize(nb);
   mlen.resize(nb);
-  // sizes (IncomingBatch::from_acquired: moves + 1 positions, or 1 for move work)
-  pool.run(nb, 2048, [&](size_t lo, size_t hi) {
+  // sizes (IncomingBatch::from_acquired: moves + 1 positions, or 1 for move
+  // work) and each batch's net; the strings are scattered in the caller's
+  // memory, so the next batches' are prefetched
+  kind.resize(nb);
+  bskip.resize(nb);
+  pool.run(nb, 256, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
+      if (i + 8 < hi) {
+        __builtin_prefetch(j.batches[i + 8].moves);
+        __builtin_prefetch(j.batches[i + 8].position);
+      }
       const fnnue_acquired& a = j.batches[i];
-      flen[i] = a.position ? (uint32_t)std::min<size_t>(std::strlen(a.position), 1u << 30) : 0;
-      mlen[i] = a.moves ? (uint32_t)std::min<size_t>(std::strlen(a.moves), 1u << 30) : 0;
+      size_t fl = a.position ? std::strlen(a.position) : 0, ml = 0;
       int rc = FNNUE_OK;
       uint32_t n = 0;
-      if (a.work == FNNUE_WORK_MOVE) n = 1;
-      else if (a.work != FNNUE_WORK_ANALYSIS) rc = FNNUE_E_ARG;
-      else if (a.nskip && !a.skip_positions) rc = FNNUE_E_ARG;
-      else n = (uint32_t)count_tokens(a.moves ? a.moves : "", mlen[i]) + 1;
+      if (a.work == FNNUE_WORK_MOVE) {
+        n = 1;
+        ml = a.moves ? std::strlen(a.moves) : 0;
+      } else if (a.work != FNNUE_WORK_ANALYSIS || (a.nskip && !a.skip_positions)) {
+        rc = FNNUE_E_ARG;
+      } else {
+        n = (uint32_t)(a.moves ? scan_tokens(a.moves, &ml) : 0) + 1;
+      }
+      flen[i] = (uint32_t)std::min<size_t>(fl, 1u << 30);
+      mlen[i] = (uint32_t)std::min<size_t>(ml, 1u << 30);
+      const int kd = kind_of(a.variant);
+      if (rc == FNNUE_OK && (kd < 0 || !ctx[kd])) rc = FNNUE_E_ARCH;  // no net for this variant on this backend
+      if (rc == FNNUE_OK && a.multipv < 0) rc = FNNUE_E_ARG;
+      kind[i] = (int8_t)kd;
+      bskip[i] = a.nskip != 0;
       j.rc[i] = rc;
-      j.off[i + 1] = rc ? 0 : n;  // counts for now, offsets below
+      j.off[i + 1] = n;  // counts for now, offsets below (a failed batch keeps its responses' place)
     }
   });
+  mark("sizes");
   j.off[0] = 0;
   for (size_t i = 0; i < nb; ++i) j.off[i + 1] += j.off[i];
   if (j.off[nb] > j.cap) {
@@ -692,56 +948,95 @@ void fnnue_backend::run(Job& j) {
     return;
   }
   for (NetWork& W : net) W.clear();
-  skip.assign(j.off[nb], 0);
+  if (skip.size() < j.off[nb]) skip.resize(j.off[nb]);  // read only for batches with bskip set
   std::vector<size_t> all_skipped;
   for (size_t i = 0; i < nb; ++i) {
-    const fnnue_acquired& a = j.batches[i];
     if (j.rc[i]) continue;
-    const int kind = kind_of(a.variant);
-    if (kind < 0 || !ctx[kind] || a.multipv < 0) {  // no net for this variant on this backend
-      j.rc[i] = kind < 0 || !ctx[kind] ? FNNUE_E_ARCH : FNNUE_E_ARG;
-      continue;
-    }
-    const uint32_t n = j.off[i + 1] - j.off[i];
+    const fnnue_acquired& a = j.batches[i];
+    const int kd = kind[i];
     if (a.work == FNNUE_WORK_MOVE) {
-      net[kind].roots.push_back(i);
+      net[kd].roots.push_back(i);
       continue;
     }
-    uint32_t live = n;
-    for (size_t q = 0; q < a.nskip; ++q)  // positions.get_mut(skip): out-of-range ids are ignored
-      if (a.skip_positions[q] < n && !skip[j.off[i] + a.skip_positions[q]]) {
-        skip[j.off[i] + a.skip_positions[q]] = 1;
-        --live;
+    if (bskip[i]) {
+      const uint32_t n = j.off[i + 1] - j.off[i];
+      uint32_t live = n;
+      std::memset(skip.data() + j.off[i], 0, n);
+      for (size_t q = 0; q < a.nskip; ++q)  // positions.get_mut(skip): out-of-range ids are ignored
+        if (a.skip_positions[q] < n && !skip[j.off[i] + a.skip_positions[q]]) {
+          skip[j.off[i] + a.skip_positions[q]] = 1;
+          --live;
+        }
+      if (!live) {
+        all_skipped.push_back(i);  // completed without the engine (IncomingError::AllSkipped)
+        continue;
       }
-    if (live) net[kind].games.push_back(i);
-    else all_skipped.push_back(i);  // completed without the engine (IncomingError::AllSkipped)
+    }
+    net[kd].games.push_back(i);
   }
+  mark("classified");
   int rc = FNNUE_OK;
+  size_t rounds = 0;
   for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k) {
     NetWork& W = net[k];
     W.rec = k == kVariantChess ? sizeof(fnnue_pos) : sizeof(fnnue_vpos);
     if (!W.roots.empty()) rc = prepare_moves(j, k);
-    if (rc == FNNUE_OK && (!W.games.empty() || W.nk)) rc = stage(j, k);
+    if (rc == FNNUE_OK && (!W.games.empty() || W.nk)) rc = plan(j, k);
+    rounds = std::max(rounds, W.pieces.size());
   }
-  const double prep_ms = ms_since(t0);
-  uint32_t syncs = 0, rebuilds = 0;
-  for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k)
-    if (net[k].pending) rc = collect(j, k, &syncs, &rebuilds);
+  mark("planned");
+  // Enqueue order: every net's first upload + replay, then each round's
+  // evaluations behind the next round's uploads (a replay runs beside the
+  // previous piece's evaluation); pieces whose results are back are written
+  // between the steps.
+  auto poll = [&](bool wait) -> int {
+    for (int k = 0; k < kKinds; ++k) {
+      NetWork& W = net[k];
+      while (W.next < W.pieces.size() && W.pieces[W.next].pending) {
+        bool ready = false;
+        if (int e = finish(j, k, wait, &ready)) return e;
+        if (!ready) break;
+      }
+    }
+    return FNNUE_OK;
+  };
+  for (size_t r = 0; r <= rounds && rc == FNNUE_OK; ++r) {
+    for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k)
+      if (r < net[k].pieces.size()) rc = stage_up(j, k, r);
+    for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k)
+      if (r >= 1 && r - 1 < net[k].pieces.size()) rc = stage_eval(k, r - 1);
+    if (rc == FNNUE_OK && r >= 1 && r < rounds) rc = poll(false);
+  }
+  for (bool left = true; rc == FNNUE_OK && left;) {
+    rc = poll(true);
+    left = false;
+    for (const NetWork& W : net) left = left || W.next < W.pieces.size();
+  }
   if (rc) {
-    for (int k = 0; k < kKinds; ++k)  // the pinned images stay in use until the copies are done
-      if (net[k].pending) (void)hipStreamSynchronize(ctx[k]->stream);
+    for (int k = 0; k < kKinds; ++k) {  // the pinned images stay in use until the copies are done
+      if (!ctx[k]) continue;
+      if (net[k].rs) (void)hipStreamSynchronize(net[k].rs);
+      (void)hipStreamSynchronize(ctx[k]->stream);
+    }
     j.ret = rc;
     j.err = g_err;
     return;
   }
-  const double dev_ms = ms_since(t0) - prep_ms;
-  const double sec = ms_since(t0) * 1e-3;
-  uint64_t evals = 0;
-  for (const NetWork& W : net) evals += W.n + W.nk;
-  const uint64_t ms = (uint64_t)(sec * 1e3);
-  const uint32_t nps = sec > 0 ? (uint32_t)std::min(4.0e9, (double)evals / sec) : 0;
-  const auto t2 = Clock::now();
-  for (int k = 0; k < kKinds; ++k) fill(j, k, ms, nps);
+  const double el = ms_since(t0);
+  const uint64_t ms = (uint64_t)el;
+  const uint32_t nps = el > 0 ? (uint32_t)std::min(4.0e9, (double)filled / (el * 1e-3)) : 0;
+  uint32_t npieces = 0;
+  for (int k = 0; k < kKinds; ++k) {
+    NetWork& W = net[k];
+    npieces += (uint32_t)W.pieces.size();
+    for (size_t t = 0; t < W.terminal.size(); ++t) {
+      fnnue_position_response& r = j.out[j.off[W.terminal[t]]];
+      std::memset(&r, 0, sizeof(r));
+      r.time_ms = ms;
+      r.nps = nps;
+      terminal_response(r, W.troots[t].fin);
+    }
+  }
   for (size_t i : all_skipped)
     for (uint32_t q = j.off[i]; q < j.off[i + 1]; ++q) {
       fnnue_position_response& r = j.out[q];
@@ -752,15 +1047,18 @@ void fnnue_backend::run(Job& j) {
       r.nps = nps;
     }
   j.ret = FNNUE_OK;
+  mark("done");
+  if (trace) std::fprintf(stderr, "FNNUE_BACKEND_TRACE {\"batches\":%zu,\"marks\":[%s]}\n", nb, tl.c_str());
   std::lock_guard<std::mutex> lk(stats_mu);
-  stats.prep_ms = prep_ms;
-  stats.device_ms = dev_ms;
-  stats.fill_ms = ms_since(t2);
   stats.total_ms = ms_since(t0);
-  stats.positions = evals;
+  stats.fill_ms = fill_ms;
+  stats.device_ms = wait_ms;
+  stats.prep_ms = stats.total_ms - fill_ms - wait_ms;
+  stats.positions = filled;
   stats.stream_syncs = syncs;
   stats.rebuilds = rebuilds;
   stats.host_threads = pool_threads;
+  stats.pieces = npieces;
 }
 
 extern "C" {
@@ -806,6 +1104,10 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
     int nt = (int)std::min(8u, hw);
     if (const char* e = std::getenv("FNNUE_BACKEND_THREADS")) nt = std::max(1, std::min(64, std::atoi(e)));
     b->pool_threads = nt;
+    b->trace = std::getenv("FNNUE_BACKEND_TRACE") != nullptr;
+    if (const char* e = std::getenv("FNNUE_BACKEND_REPLAY_CUS")) b->replay_cus = std::max(0, std::atoi(e));
+    b->replay_serial = std::getenv("FNNUE_BACKEND_REPLAY_SERIAL") != nullptr;
+    if (const char* e = std::getenv("FNNUE_BACKEND_PIECE_PLIES")) b->piece_plies = (size_t)std::max(1024L, std::atol(e));
   }
   for (int k = 0; k < kKinds; ++k) {
     if (!slot[k]) continue;

@@ -506,60 +506,79 @@ struct ChessRules {
     const uint32_t v = (cr >> (8 * (2 * c + side))) & 0xFFu;
     return v == 0xFFu ? -1 : (int)v;
   }
-  // The move the code names if it names one: castling when the own king goes
-  // to a castling rook's square or (standard positions) to its two-square
-  // destination; everything else as written (en passant and double pushes
-  // are do_move's business).  verify() decides whether it is legal.
-  __device__ static bool interpret(const Scalars& b, uint32_t code, DMove& m, uint32_t sqv) {
-    const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
-    const uint32_t pc = replay::lane_value(sqv, from);
-    if (!pc || (int)(pc >> 3) != (int)b.stm) return false;
-    m = DMove{from, to, promo, 0};
-    if ((pc & 7) == KING && !promo) {
-      const int back = b.stm == WHITE ? 0 : 56;
-#pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const int rsq = sc_cr(b.cr, b.stm, side);
-        if (rsq >= 0 && (to == rsq || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) {
-          m = DMove{from, rsq, 0, 1};
-          return true;
-        }
-      }
-    }
-    return true;
+  // Along the chain cr and ep change; stm alternates and c960 is fixed, so
+  // the checking lanes derive those two from the window's first scalars.
+  static constexpr int kVary = 2;
+  __device__ static void fix(Scalars& s, const Scalars& s0, uint32_t plies) {
+    s.stm = s0.stm ^ (plies & 1u);
+    s.c960 = s0.c960;
   }
   __device__ static uint32_t lane_square(const DBoard& b, int sq) { return (uint32_t)piece_at(b, sq); }
-  // do_move with lane l holding square l's piece code: every square the move
-  // changes is one select per lane, the rest is the scalars.
-  __device__ static void play(Scalars& b, const DMove& m, uint32_t& sqv, int lane) {
-    const int us = b.stm;
-    const int pc = (int)replay::lane_value(sqv, m.from);
+  // does a byte of the packed castling rooks name square v (0xFF never does)
+  __device__ static bool cr_names(uint32_t cr, uint32_t v) {
+    const uint32_t t = cr ^ (v * 0x01010101u);
+    return ((t - 0x01010101u) & ~t & 0x80808080u) != 0;
+  }
+  // One chain step: the move the code names, played on the lane bytes (lane
+  // l holds square l's piece code) and the scalars; returns it packed.  It is
+  // castling when the own king goes to a castling rook's square or
+  // (standard positions) to its two-square destination; everything else as
+  // written.  Nothing is checked here: verify() tests the move against the
+  // board before it (a code that names no move of the side to move fails
+  // there, at its own ply — and a failed ply ends the game's replay).
+  __device__ __forceinline__ static bool step(Scalars& b, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv) {
+    const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
+    const int us = (int)b.stm;
+    const uint32_t pc = replay::lane_value(sqv, from);
     const int back = us == WHITE ? 0 : 56;
     uint32_t v = sqv;
     int new_ep = -1;
-    if (m.castle) {
-      const bool king_side = m.to > m.from;
-      const int kto = back + (king_side ? 6 : 2), rto = back + (king_side ? 5 : 3);
-      v = (lane == m.from || lane == m.to) ? 0u : v;
-      v = lane == kto ? (uint32_t)pc : v;
-      v = lane == rto ? (uint32_t)make_piece_d(us, ROOK) : v;
-      b.cr |= 0xFFFFu << (16 * us);
+    mv = (uint32_t)from | ((uint32_t)to << 6) | ((uint32_t)promo << 12);
+    if ((pc & 7) == KING) {  // castling, or a king move: the mover's rights go
+      int rsq = -1;
+      if (!promo) {
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          const int r = sc_cr(b.cr, us, side);
+          if (rsq < 0 && r >= 0 && (to == r || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) rsq = r;
+        }
+      }
+      if (rsq >= 0) {
+        const bool king_side = rsq > from;
+        const int kto = back + (king_side ? 6 : 2), rto = back + (king_side ? 5 : 3);
+        v = (lane == from || lane == rsq) ? 0u : v;
+        v = lane == kto ? pc : v;
+        v = lane == rto ? (uint32_t)make_piece_d(us, ROOK) : v;
+        mv = (uint32_t)from | ((uint32_t)rsq << 6) | (1u << 15);
+        b.cr |= 0xFFFFu << (16 * us);
+      } else {
+        v = lane == from ? 0u : v;
+        v = lane == to ? (promo ? (uint32_t)make_piece_d(us, promo) : pc) : v;
+        b.cr |= 0xFFFFu << (16 * us);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t r = (b.cr >> (8 * i)) & 0xFFu;
+          if (r == (uint32_t)from || r == (uint32_t)to) b.cr |= 0xFFu << (8 * i);
+        }
+      }
     } else {
       const bool pawn = (pc & 7) == PAWN;
-      const int cap = (pawn && m.to == b.ep && (m.from & 7) != (m.to & 7)) ? m.to + (us == WHITE ? -8 : 8) : -1;
-      v = (lane == m.from || lane == cap) ? 0u : v;
-      v = lane == m.to ? (uint32_t)(m.promo ? make_piece_d(us, m.promo) : pc) : v;
-      if (pawn && (m.from ^ m.to) == 16) new_ep = (m.from + m.to) / 2;
-      if ((pc & 7) == KING) b.cr |= 0xFFFFu << (16 * us);
+      const int cap = (pawn && to == b.ep && ((from ^ to) & 7)) ? to + (us == WHITE ? -8 : 8) : -1;
+      v = (lane == from || lane == cap) ? 0u : v;
+      v = lane == to ? (promo ? (uint32_t)make_piece_d(us, promo) : pc) : v;
+      if (pawn && (from ^ to) == 16) new_ep = (from + to) >> 1;
+      if (cr_names(b.cr, (uint32_t)from) || cr_names(b.cr, (uint32_t)to)) {  // a castling rook moves or is taken
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t r = (b.cr >> (8 * i)) & 0xFFu;
-        if (r == (uint32_t)m.from || r == (uint32_t)m.to) b.cr |= 0xFFu << (8 * i);
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t r = (b.cr >> (8 * i)) & 0xFFu;
+          if (r == (uint32_t)from || r == (uint32_t)to) b.cr |= 0xFFu << (8 * i);
+        }
       }
     }
     sqv = v;
     b.ep = new_ep;
     b.stm = (uint32_t)(us ^ 1);
+    return true;
   }
   __device__ static uint32_t pack_move(const DMove& m) {
     return (uint32_t)m.from | ((uint32_t)m.to << 6) | ((uint32_t)m.promo << 12) | ((uint32_t)m.castle << 15);

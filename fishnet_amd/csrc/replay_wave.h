@@ -20,7 +20,8 @@
 //       makes) — and packs the board after it into the output record,
 // and repeats until the game's text is consumed.  The first move whose check
 // fails ends the game with a latched error (the batch fails: PositionFailed);
-// boards after it are never written.  The last board gets the game-end flags
+// records after it (inside the game's own range) are meaningless, the game
+// is dropped.  The last board gets the game-end flags
 // (no legal move / check / exploded king), its legal-move search split over
 // the lanes by from-square.
 //
@@ -137,13 +138,17 @@ __device__ __forceinline__ void pack_nibbles(const uint32_t (&w)[16], uint32_t (
 //                                                       the standard start (< 64 characters) and its board
 //   uint32_t encode(const char* c, int len)             token -> code (kTokBad if malformed)
 //   Scalars scalars(const Board&); uint32_t lane_square(const Board&, int sq)
-//   bool interpret(const Scalars&, uint32_t code, Move&, uint32_t sqv)
-//                                                       cheap: the move the code would be
-//   void play(Scalars&, const Move&, uint32_t& sqv, int lane)  do_move on the lane bytes
-//   uint32_t pack_move(const Move&); Move unpack_move(uint32_t)
+//   bool step(Scalars&, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv)
+//                                                       one chain step: the move the code names, played on
+//                                                       the lane bytes; mv = that move packed (false: the
+//                                                       code names none, the replay stops there)
+//   kVary; void fix(Scalars&, const Scalars& s0, uint32_t plies)
+//                                                       the first kVary words change along the chain; fix
+//                                                       sets the rest from the window's first scalars
+//   Move unpack_move(uint32_t)
 //   Board board_from(const uint32_t (&w)[16], const Scalars&)   snapshot -> board (per lane)
 //   Pos pack_from(const uint32_t (&w)[16], const Scalars&)      snapshot -> record (per lane)
-//   bool verify(const Board&, const Move&)              the move interpret() built is legal
+//   bool verify(const Board&, const Move&)              the move step() played is legal
 //   Pos pack(const Board&)
 //   bool any_legal_from(const Board&, int sq, bool drops) legal moves of the piece on sq (+ drops)
 //   uint8_t end_flags(const Board&, bool any)             kFinal* of a last position
@@ -156,7 +161,6 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
                                                          typename R::Board* __restrict__ states,
                                                          uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
   using Board = typename R::Board;
-  using Move = typename R::Move;
   using Sc = typename R::Scalars;
   constexpr int kScw = sizeof(Sc) / 4;
   static_assert(sizeof(Sc) % 4 == 0, "scalars as dwords");
@@ -269,43 +273,51 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     // collects move j's code, the move and the scalars after it,
     // SNAP[j + 1] the board after it.
     const uint32_t myc = TK[lane];
+    // the codes are in registers before the chain starts, so the loop head
+    // waits for nothing (its only LDS access is the snapshot byte store)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(myc) : "memory");
     const Sc sc0 = sc;
     uint32_t mvw = 0;
-    uint32_t scw[kScw];
+    uint32_t scw[R::kVary];
 #pragma unroll
-    for (int w = 0; w < kScw; ++w) scw[w] = 0;
+    for (int w = 0; w < R::kVary; ++w) scw[w] = 0;
     uint32_t kplay = k;
     for (uint32_t j = 0; j < k; ++j) {
       const uint32_t code = lane_value(myc, (int)j);
-      Move m;
-      if ((code & kTokBad) || !R::interpret(sc, code, m, sqv)) {
+      uint32_t mv;
+      if ((code & kTokBad) || !R::step(sc, code, sqv, lane, mv)) {
         kplay = j;
         break;
       }
-      R::play(sc, m, sqv, lane);
       reinterpret_cast<uint8_t*>(SNAP[j + 1])[lane] = (uint8_t)sqv;
       const bool mine = (uint32_t)lane == j;
-      mvw = mine ? R::pack_move(m) : mvw;
+      mvw = mine ? mv : mvw;
       uint32_t cur[kScw];
       __builtin_memcpy(cur, &sc, sizeof(Sc));
 #pragma unroll
-      for (int w = 0; w < kScw; ++w) scw[w] = mine ? cur[w] : scw[w];
+      for (int w = 0; w < R::kVary; ++w) scw[w] = mine ? cur[w] : scw[w];
     }
     lds_fence();
     // (c) lane j checks move j against the board before it and packs the board after it
     bool fail = false;
     {
-      uint32_t sb[kScw], s0[kScw];
-      __builtin_memcpy(s0, &sc0, sizeof(Sc));
+      // scalars before move j: after move j - 1, or the window's own; the
+      // words the chain does not collect follow from the window's first
+      uint32_t sb[kScw], sa[kScw];
+      __builtin_memcpy(sb, &sc0, sizeof(Sc));
+      __builtin_memcpy(sa, &sc0, sizeof(Sc));
 #pragma unroll
-      for (int w = 0; w < kScw; ++w) {  // scalars before move j: after move j - 1, or the window's own
+      for (int w = 0; w < R::kVary; ++w) {
         const uint32_t up = (uint32_t)__shfl_up((int)scw[w], 1, 64);
-        sb[w] = lane == 0 ? s0[w] : up;
+        sb[w] = lane == 0 ? sb[w] : up;
+        sa[w] = scw[w];
       }
       if ((uint32_t)lane < kplay) {
         Sc before_sc, after_sc;
         __builtin_memcpy(&before_sc, sb, sizeof(Sc));
-        __builtin_memcpy(&after_sc, scw, sizeof(Sc));
+        __builtin_memcpy(&after_sc, sa, sizeof(Sc));
+        R::fix(before_sc, sc0, (uint32_t)lane);
+        R::fix(after_sc, sc0, (uint32_t)lane + 1);
         uint32_t wb[16], wa[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {

@@ -46,6 +46,13 @@ struct VariantRules {
     uint32_t stm;
     uint32_t vc;
   };
+  // Along the chain the pockets, cr and ep change; stm alternates and the
+  // variant word is fixed (the checking lanes derive those two).
+  static constexpr int kVary = 6;
+  __device__ static void fix(Scalars& s, const Scalars& s0, uint32_t plies) {
+    s.stm = s0.stm ^ (plies & 1u);
+    s.vc = s0.vc;
+  }
   __device__ static Scalars scalars(const vb::VBoard& b) {
     Scalars s;
     s.pocket[0] = b.pocket[0];
@@ -215,6 +222,15 @@ struct VariantRules {
     }
     b.ep = new_ep;
     b.stm = (uint32_t)(us ^ 1);
+  }
+  // One chain step: interpret the code on the current board and play it;
+  // false: it names no move of the side to move (the game's replay ends).
+  __device__ __forceinline__ static bool step(Scalars& b, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv) {
+    vb::VMove m;
+    if (!interpret(b, code, m, sqv)) return false;
+    play(b, m, sqv, lane);
+    mv = pack_move(m);
+    return true;
   }
   __device__ static uint32_t pack_move(const vb::VMove& m) {
     uint32_t w;

@@ -100,8 +100,8 @@ typedef struct {
   int32_t psqt;          /* the raw NNUE terms the score came from */
   int32_t positional;
   uint64_t nodes;
-  uint64_t time_ms;      /* wall time of the go() call */
-  uint32_t nps;          /* positions evaluated per second over the go() call */
+  uint64_t time_ms;      /* wall time of the go() call until this position's piece was back on the host */
+  uint32_t nps;          /* positions evaluated by then, per second */
   char best_move[8];     /* UCI, NUL-terminated; "" for analysis */
 } fnnue_position_response;
 
@@ -136,19 +136,22 @@ int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nba
                      size_t cap, uint32_t *off, int32_t *batch_rc);
 
 /* Where the last go() spent its time (diagnostics; the reference's engine
- * reports only time / nps per position).  One net's work is one host-to-
- * device copy, the replay and evaluation kernels, one device-to-host copy of
- * the results and of the evaluator's error word, and one wait. */
+ * reports only time / nps per position).  Each net's games are cut into pieces
+ * of about FNNUE_BACKEND_PIECE_PLIES plies (default 262144); a piece is one
+ * host-to-device copy, the replay, the evaluation kernels and one device-to-
+ * host copy of its results (plus the evaluator's error word).  The next
+ * piece's copy and replay run beside this piece's evaluation, and the host
+ * writes a piece's responses while the device works on the later ones. */
 typedef struct {
   double prep_ms;         /* host: sizes, move-work roots, text staging, copies and kernels enqueued */
-  double device_ms;       /* from then until every net's results are on the host */
-  double fill_ms;         /* responses written */
+  double device_ms;       /* host blocked waiting for the device */
+  double fill_ms;         /* responses written (overlaps the device's later pieces) */
   double total_ms;
   uint64_t positions;     /* positions evaluated (analysis plies + move-work children) */
-  uint32_t stream_syncs;  /* host waits on a stream or a blocking copy */
-  uint32_t rebuilds;      /* extra passes after a batch failed (per failed batch, its net only) */
+  uint32_t stream_syncs;  /* host waits on an event, a stream or a blocking copy */
+  uint32_t rebuilds;      /* extra passes after a batch failed (per failed batch, its piece only) */
   uint32_t host_threads;  /* threads for the staging / fill loops (FNNUE_BACKEND_THREADS, default <= 8) */
-  uint32_t reserved;
+  uint32_t pieces;        /* pieces over all nets */
 } fnnue_backend_stats;
 
 int fnnue_backend_last_stats(fnnue_backend *b, fnnue_backend_stats *out);

@@ -92,3 +92,28 @@ def test_channel_nets_slot_checks_without_a_device():
                        ((None, None, zh._h), -4)):
         rc = N.lib.fnnue_backend_channel_nets(C.byref(B._Nets(*nets)), 0, None, C.byref(h))
         assert rc == code, (nets, rc)
+
+
+def test_batch_size_counts_tokens_like_the_builder():
+    """fnnue_backend_batch_size counts the moves with the 16-byte scan
+    (blanks ' ', tab, newline, CR): against Python's split on random texts of
+    every length 0..80 at every start alignment 0..15 of the buffer."""
+    import ctypes as C
+    import random
+    rng = random.Random(5)
+    blanks = " \t\n\r"
+    for length in range(81):
+        text = "".join(rng.choice("e2e4q" + blanks) if rng.random() < 0.7 else rng.choice(blanks)
+                       for _ in range(length))
+        raw = text.encode()
+        for shift in range(16):
+            buf = C.create_string_buffer(64 + len(raw) + 1)
+            base = (-C.addressof(buf)) % 16  # first 16-byte aligned offset
+            C.memmove(C.addressof(buf) + base + shift, raw + b"\0", len(raw) + 1)
+            a = B._Acquired()
+            a.work = 0  # FNNUE_WORK_ANALYSIS
+            a.position = START.encode()
+            a.moves = C.cast(C.addressof(buf) + base + shift, C.c_char_p)
+            n = C.c_size_t()
+            N.check(N.lib.fnnue_backend_batch_size(C.byref(a), C.byref(n)))
+            assert n.value == len(text.split()) + 1, (repr(text), shift)

@@ -375,3 +375,59 @@ def test_every_variant_token_matches_the_host_builder(chan):
         assert rc == 0
         got = np.array([(res[i][1].psqt, res[i][1].positional) for i in ok])
         assert np.array_equal(got[:, 0], ps) and np.array_equal(got[:, 1], po)
+
+
+def test_pieces_with_failures_in_between(monkeypatch):
+    """Small pieces (FNNUE_BACKEND_PIECE_PLIES = 1024): a call spans several
+    pieces per net, overlapping uploads / replays / evaluations / fills; a
+    builder failure and an evaluator failure (a position with more than 32
+    pieces, the evaluator's sticky error word) inside middle pieces fail their
+    own batches only, every other batch bit-exact, move work in the net's last
+    piece."""
+    monkeypatch.setenv("FNNUE_BACKEND_PIECE_PLIES", "1024")
+    data = net_bytes(1, 1024, 0)
+    zh = F.synthesize_variant_net(5, 512, ZH)
+    stub, actor = B.channel(F.Net.from_bytes(data), 0, crazyhouse=F.Net.from_bytes_variant(zh, ZH))
+    on = {0: OracleNet(data), ZH: VariantOracleNet(zh, ZH)}
+    crowded = "rnbqkbnr/pppppppp/pppppppp/8/8/PPPPPPPP/PPPPPPPP/RNBQKBNR w - - 0 1"
+    try:
+        bodies, kinds = [], []
+        for i, g in enumerate(GAMES[:80]):
+            bodies.append(B.AcquireResponseBody(str(g["id"]), g["position"], g["moves"]))
+            kinds.append(0)
+            if i in (25, 50):
+                bodies.append(B.AcquireResponseBody(f"bad{i}", START, "e2e4 e7e5 e1e3"))
+                kinds.append(-1)
+            if i == 40:
+                bodies.append(B.AcquireResponseBody("crowded", crowded, "a3a4"))
+                kinds.append(-1)
+            if i % 8 == 0:
+                bodies.append(B.AcquireResponseBody(f"zh{i}", ZH_START, F.random_vgame(77 + i, ZH, ZH_START, 60 + i),
+                                                    variant="crazyhouse"))
+                kinds.append(ZH)
+        bodies.append(B.AcquireResponseBody("mv", GAMES[0]["position"], " ".join(GAMES[0]["moves"].split()[:20]),
+                                            work="move"))
+        kinds.append(-2)
+        res = stub.go(bodies)
+        st = B.last_stats(actor)
+        assert st["pieces"] >= 5, st
+        assert st["rebuilds"] >= 2, st
+        for b, rows, kind in zip(bodies, res, kinds):
+            if kind == -1:
+                assert isinstance(rows, B.PositionFailed), b.batch_id
+            elif kind == -2:
+                kids, ps, po = search1(on, b.position, b.moves)
+                vals = [-int((int(x) + int(y)) / 16) for x, y in zip(ps, po)]
+                assert rows[0].nodes == len(kids) and rows[0].score == B.Score("cp", int(max(vals) * 100 / 361))
+            else:
+                assert not isinstance(rows, B.PositionFailed), (b.batch_id, rows)
+                check_rows(on, b, rows, kind)
+        # the same call again: pieces and buffers reused, results unchanged
+        again = stub.go(bodies)
+        for a, r in zip(res, again):
+            if isinstance(a, B.PositionFailed):
+                assert isinstance(r, B.PositionFailed) and r.code == a.code
+            else:
+                assert [(x.psqt, x.positional, x.score) for x in a] == [(x.psqt, x.positional, x.score) for x in r]
+    finally:
+        actor.close()
