@@ -15,15 +15,14 @@
 // response offsets are part of the answer) and cuts the games into pieces;
 // per piece it stages the text, offsets (and, in the last piece, the
 // move-work children) in a pinned image and sends it with one copy; the
-// net's replay stream runs the replay (one wave per game), the context's
-// stream the CHAIN evaluation and the children's evaluation, and one copy
-// brings back the builder's error word, the game-end flags and every (psqt,
-// positional).  Pieces overlap: the next piece's copy and replay run beside
-// this one's evaluation, and the host writes a piece's responses while the
-// device works on the later ones.  Buffers are grow-only (device and pinned
-// host), so a steady stream of calls allocates nothing.  A failed batch costs
-// a second pass for its piece only.  Large calls spread the host work (text
-// staging, response fill) over a few threads.
+// context's stream runs the replay (one wave per game), the CHAIN evaluation
+// and the children's evaluation, and one copy brings back the builder's error
+// word, the game-end flags and every (psqt, positional).  The nets' streams
+// run side by side, and the host stages the next pieces and writes a piece's
+// responses while the device works on the later ones.  Buffers are grow-only
+// (device and pinned host), so a steady stream of calls allocates nothing.  A
+// failed batch costs a second pass for its piece only.  Large calls spread the
+// host work (text staging, response fill) over a few threads.
 #include "../../include/fnnue_backend.h"
 
 #include <algorithm>
@@ -342,11 +341,12 @@ struct Piece {
 };
 
 // One net's share of a go(): its analysis games cut into pieces of about
-// piece_plies plies, and its move-work roots.  A piece's upload and replay run
-// on the net's replay stream, its evaluation and download on the context's
-// stream (after the replay's event): the next piece's upload and replay
-// overlap this piece's evaluation, and the host writes a piece's responses
-// while the device works on the later ones.
+// piece_plies plies, and its move-work roots.  A piece's upload, replay,
+// evaluation and download run on the context's stream, one piece after the
+// other; the host stages the next pieces and writes a piece's responses while
+// the device works on the later ones.  (The replay of the next piece on a
+// stream of its own, beside this piece's evaluation, measured slower: its
+// waves hold CU slots the evaluation's 1024-thread workgroups need.)
 struct NetWork {
   std::vector<size_t> games;      // analysis batches (job indices)
   std::vector<size_t> roots;      // move batches whose roots have legal children
@@ -358,8 +358,7 @@ struct NetWork {
   std::vector<Piece> pieces;
   size_t nk = 0, rec = 0;
   size_t next = 0;                // first piece whose responses are not written yet
-  hipStream_t rs = nullptr;       // replay stream
-  std::vector<hipEvent_t> ev_up, ev_done;  // per piece: replayed; results and error word on the host
+  std::vector<hipEvent_t> ev_done;  // per piece: results and error word on the host
   DevBuf dev, pos;
   PinnedBuf up, down, cerr;
   void clear() {
@@ -375,15 +374,10 @@ struct NetWork {
     next = 0;
   }
   int events(size_t n) {
-    while (ev_up.size() < n) {
-      hipEvent_t a = nullptr, b = nullptr;
-      if (hipEventCreateWithFlags(&a, hipEventDisableTiming) != hipSuccess) return fail(FNNUE_E_DEVICE, "hipEventCreate");
-      if (hipEventCreateWithFlags(&b, hipEventDisableTiming) != hipSuccess) {
-        (void)hipEventDestroy(a);
-        return fail(FNNUE_E_DEVICE, "hipEventCreate");
-      }
-      ev_up.push_back(a);
-      ev_done.push_back(b);
+    while (ev_done.size() < n) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FNNUE_E_DEVICE, "hipEventCreate");
+      ev_done.push_back(e);
     }
     return FNNUE_OK;
   }
@@ -393,12 +387,8 @@ struct NetWork {
     up.release();
     down.release();
     cerr.release();
-    for (hipEvent_t e : ev_up) (void)hipEventDestroy(e);
     for (hipEvent_t e : ev_done) (void)hipEventDestroy(e);
-    ev_up.clear();
     ev_done.clear();
-    if (rs) (void)hipStreamDestroy(rs);
-    rs = nullptr;
   }
 };
 
@@ -410,9 +400,7 @@ struct fnnue_backend {
   fnnue_ctx* ctx[kKinds] = {};  // one evaluator per net, all on one device
   int device = 0;
   int32_t norm = kNormalizeToPawnSf151;
-  size_t piece_plies = 262144;  // FNNUE_BACKEND_PIECE_PLIES
-  int replay_cus = 0;           // FNNUE_BACKEND_REPLAY_CUS: > 0 = the replay stream on that many CUs
-  bool replay_serial = false;   // FNNUE_BACKEND_REPLAY_SERIAL: replay on the evaluation stream
+  size_t piece_plies = 524288;  // FNNUE_BACKEND_PIECE_PLIES
   std::thread th;
   std::mutex mu;
   std::condition_variable cv;  // slot / done / stop changes
@@ -576,29 +564,10 @@ int fnnue_backend::plan(Job& j, int k) {
   if (int rc = W.cerr.reserve(4 * W.pieces.size())) return rc;
   if (pos)
     if (int rc = W.pos.reserve(pos)) return rc;
-  if (!W.rs) {
-    if (replay_serial) {
-      W.rs = nullptr;
-    } else if (replay_cus > 0) {
-      // the replay's waves on replay_cus CUs spread over the device (the
-      // evaluation keeps the others): one mask bit per CU
-      int ncu = 0;
-      HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "hipDeviceGetAttribute");
-      std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
-      const int use = std::min(replay_cus, ncu);
-      for (int i = 0; i < use; ++i) {
-        const int cu = (int)((int64_t)i * ncu / use);
-        mask[(size_t)cu / 32] |= 1u << (cu % 32);
-      }
-      HIP_TRY(hipExtStreamCreateWithCUMask(&W.rs, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
-    } else {
-      HIP_TRY(hipStreamCreateWithFlags(&W.rs, hipStreamNonBlocking), "hipStreamCreate(replay)");
-    }
-  }
   return W.events(W.pieces.size());
 }
 
-// Host image of a piece, then on the replay stream: its upload and the
+// Host image of a piece, then on the context's stream: its upload and the
 // replay of its games.  Nothing waits.
 int fnnue_backend::stage_up(Job& j, int k, size_t pi) {
   NetWork& W = net[k];
@@ -632,7 +601,7 @@ int fnnue_backend::stage_up(Job& j, int k, size_t pi) {
   if (P.nk) std::memcpy(img + P.o_kids, W.kids.data(), P.nk * W.rec);
   std::memset(img + P.o_res, 0, 16);
   char* dimg = W.dev.at<char>(P.dev0);
-  hipStream_t us = W.rs ? W.rs : ctx[k]->stream;
+  hipStream_t us = ctx[k]->stream;
   HIP_TRY(hipMemcpyAsync(dimg, img, P.o_res + 16, hipMemcpyHostToDevice, us), "H2D(batch image)");
   if (P.ng)
     HIP_TRY(replay_games_device(k, dimg, reinterpret_cast<uint32_t*>(dimg + P.o_fen),
@@ -640,12 +609,11 @@ int fnnue_backend::stage_up(Job& j, int k, size_t pi) {
                                 P.ng, W.pos.at<char>(P.pos0), reinterpret_cast<uint8_t*>(dimg + P.o_fin),
                                 reinterpret_cast<uint32_t*>(dimg + P.o_res), us),
             "batch replay launch");
-  HIP_TRY(hipEventRecord(W.ev_up[pi], us), "hipEventRecord(replayed)");
   mark("up", k, (long)pi);
   return FNNUE_OK;
 }
 
-// On the context's stream, after the piece's replay: the CHAIN evaluation of
+// On the context's stream, behind the piece's replay: the CHAIN evaluation of
 // its plies, the children's evaluation, the results and the evaluator's error
 // word to the host.  Nothing waits.
 int fnnue_backend::stage_eval(int k, size_t pi) {
@@ -657,7 +625,6 @@ int fnnue_backend::stage_eval(int k, size_t pi) {
   char* dimg = W.dev.at<char>(P.dev0);
   int32_t* d_ps = reinterpret_cast<int32_t*>(dimg + P.o_ps);
   int32_t* d_po = reinterpret_cast<int32_t*>(dimg + P.o_po);
-  HIP_TRY(hipStreamWaitEvent(s, W.ev_up[pi], 0), "hipStreamWaitEvent(replayed)");
   if (P.ng) {
     const uint32_t* d_off = reinterpret_cast<const uint32_t*>(dimg + P.o_ply);
     const void* d_pos = W.pos.at<char>(P.pos0);
@@ -722,9 +689,8 @@ int fnnue_backend::recover(Job& j, int k, size_t pi) {
   fnnue_ctx* c = ctx[k];
   hipStream_t s = c->stream;
   Piece& P = W.pieces[pi];
-  if (W.rs) HIP_TRY(hipStreamSynchronize(W.rs), "hipStreamSynchronize(replay)");
   HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-  syncs += 2;
+  ++syncs;
   // The drain also ran the evaluations enqueued behind this piece: whatever
   // they latched is cleared here, and they are staged again below.
   HIP_TRY(hipMemsetAsync(c->err, 0, 4, s), "hipMemsetAsync(error word)");
@@ -985,10 +951,9 @@ void fnnue_backend::run(Job& j) {
     rounds = std::max(rounds, W.pieces.size());
   }
   mark("planned");
-  // Enqueue order: every net's first upload + replay, then each round's
-  // evaluations behind the next round's uploads (a replay runs beside the
-  // previous piece's evaluation); pieces whose results are back are written
-  // between the steps.
+  // Enqueue order: every net's first upload + replay (the nets' streams run
+  // side by side), then each round's evaluations behind the next round's
+  // uploads; pieces whose results are back are written between the steps.
   auto poll = [&](bool wait) -> int {
     for (int k = 0; k < kKinds; ++k) {
       NetWork& W = net[k];
@@ -1015,7 +980,6 @@ void fnnue_backend::run(Job& j) {
   if (rc) {
     for (int k = 0; k < kKinds; ++k) {  // the pinned images stay in use until the copies are done
       if (!ctx[k]) continue;
-      if (net[k].rs) (void)hipStreamSynchronize(net[k].rs);
       (void)hipStreamSynchronize(ctx[k]->stream);
     }
     j.ret = rc;
@@ -1105,8 +1069,6 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
     if (const char* e = std::getenv("FNNUE_BACKEND_THREADS")) nt = std::max(1, std::min(64, std::atoi(e)));
     b->pool_threads = nt;
     b->trace = std::getenv("FNNUE_BACKEND_TRACE") != nullptr;
-    if (const char* e = std::getenv("FNNUE_BACKEND_REPLAY_CUS")) b->replay_cus = std::max(0, std::atoi(e));
-    b->replay_serial = std::getenv("FNNUE_BACKEND_REPLAY_SERIAL") != nullptr;
     if (const char* e = std::getenv("FNNUE_BACKEND_PIECE_PLIES")) b->piece_plies = (size_t)std::max(1024L, std::atol(e));
   }
   for (int k = 0; k < kKinds; ++k) {

@@ -455,12 +455,26 @@ struct ChessRules {
   using Board = DBoard;
   using Move = DMove;
   using Pos = fnnue_pos;
-  // the board's non-square state: castling rooks (DBoard::cr packing), en passant, side to move
+  // The board's non-square state.  The chain keeps en passant and the side to
+  // move; castling rights are not kept along it: a right (colour c, side) is
+  // alive while neither its rook's square nor c's king square at the game's
+  // start has been touched (a from / to square of any move so far: the king
+  // moved, the rook moved or was taken — DBoard::cr's update rule), so with
+  // the squares the game's moves touch (m: before the window; a window's own
+  // by a lane-parallel prefix OR) every ply's rights follow from the start's.
   struct Scalars {
-    uint32_t cr;
     int32_t ep;
     uint32_t stm;
     uint32_t c960;
+    uint32_t cr;    // derived: the rights for m (window starts, last board) or per checking lane
+    uint32_t cr0;   // the start's castling rooks (DBoard::cr packing)
+    uint32_t ksq;   // the start's king squares, white | black << 8 (64: none)
+    uint32_t mlo, mhi;  // squares touched before the window
+  };
+  // per window, per lane j: the touched squares before move j (m included)
+  // and move j's own
+  struct Win {
+    uint64_t pre, own;
   };
   __device__ static bool parse_fen(const char* t, uint32_t p, uint32_t e, int, DBoard& b) {
     return fnnue::parse_fen(t, p, e, b);
@@ -501,32 +515,72 @@ struct ChessRules {
     }
     return (uint32_t)from | ((uint32_t)to << 6) | (promo << 12);
   }
-  __device__ static Scalars scalars(const DBoard& b) { return Scalars{b.cr, b.ep, b.stm, b.c960}; }
+  __device__ static Scalars scalars(const DBoard& b) {
+    const uint64_t wk = b.bc[WHITE] & b.bt[KING], bk = b.bc[BLACK] & b.bt[KING];
+    const uint32_t k0 = wk ? (uint32_t)__builtin_ctzll(wk) : 64u, k1 = bk ? (uint32_t)__builtin_ctzll(bk) : 64u;
+    return Scalars{b.ep, b.stm, b.c960, b.cr, b.cr, k0 | k1 << 8, 0u, 0u};
+  }
   __device__ static int sc_cr(uint32_t cr, int c, int side) {
     const uint32_t v = (cr >> (8 * (2 * c + side))) & 0xFFu;
     return v == 0xFFu ? -1 : (int)v;
   }
-  // Along the chain cr and ep change; stm alternates and c960 is fixed, so
-  // the checking lanes derive those two from the window's first scalars.
-  static constexpr int kVary = 2;
-  __device__ static void fix(Scalars& s, const Scalars& s0, uint32_t plies) {
-    s.stm = s0.stm ^ (plies & 1u);
+  __device__ static bool touched(uint64_t m, uint32_t sq) { return sq < 64 && ((m >> sq) & 1u); }
+  // the castling rooks still alive after the squares m were touched
+  __device__ static uint32_t rights(uint32_t cr0, uint32_t ksq, uint64_t m) {
+    uint32_t cr = cr0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = (cr0 >> (8 * i)) & 0xFFu, k = (ksq >> (8 * (i >> 1))) & 0xFFu;
+      if (r == 0xFFu || touched(m, r) || touched(m, k)) cr |= 0xFFu << (8 * i);
+    }
+    return cr;
+  }
+  // Before the chain: each lane's move squares and the exclusive prefix OR of
+  // the window's (k moves) in front of it, m included.
+  __device__ static Win window(const Scalars& sc, uint32_t code, uint32_t k, int lane) {
+    uint64_t own = 0;
+    if ((uint32_t)lane < k && !(code & replay::kTokBad))
+      own = (1ull << replay::tok_from(code)) | (1ull << replay::tok_to(code));
+    uint32_t lo = (uint32_t)own, hi = (uint32_t)(own >> 32);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // inclusive prefix OR
+      const uint32_t ulo = (uint32_t)__shfl_up((int)lo, o, 64), uhi = (uint32_t)__shfl_up((int)hi, o, 64);
+      if (lane >= o) {
+        lo |= ulo;
+        hi |= uhi;
+      }
+    }
+    uint32_t elo = (uint32_t)__shfl_up((int)lo, 1, 64), ehi = (uint32_t)__shfl_up((int)hi, 1, 64);
+    if (lane == 0) elo = ehi = 0;
+    return Win{((uint64_t)elo | (uint64_t)ehi << 32) | ((uint64_t)sc.mlo | (uint64_t)sc.mhi << 32), own};
+  }
+  // After a window of k moves: m and the rights for the board after them.
+  __device__ static void advance(Scalars& sc, const Win& w, uint32_t k) {
+    const uint64_t m = replay::lane_u64(w.pre, (int)k - 1) | replay::lane_u64(w.own, (int)k - 1);
+    sc.mlo = (uint32_t)m;
+    sc.mhi = (uint32_t)(m >> 32);
+    sc.cr = rights(sc.cr0, sc.ksq, m);
+  }
+  // Along the chain only ep changes (collected per lane); the checking lane of
+  // move j derives the rest: stm by parity, the rights from the squares
+  // touched before move j (after: and by it).
+  static constexpr int kVary = 1;
+  __device__ static void fix(Scalars& s, const Scalars& s0, const Win& w, uint32_t j, bool after) {
+    s.stm = s0.stm ^ ((j + (after ? 1u : 0u)) & 1u);
     s.c960 = s0.c960;
+    s.cr = rights(s0.cr0, s0.ksq, after ? w.pre | w.own : w.pre);
   }
   __device__ static uint32_t lane_square(const DBoard& b, int sq) { return (uint32_t)piece_at(b, sq); }
-  // does a byte of the packed castling rooks name square v (0xFF never does)
-  __device__ static bool cr_names(uint32_t cr, uint32_t v) {
-    const uint32_t t = cr ^ (v * 0x01010101u);
-    return ((t - 0x01010101u) & ~t & 0x80808080u) != 0;
-  }
-  // One chain step: the move the code names, played on the lane bytes (lane
-  // l holds square l's piece code) and the scalars; returns it packed.  It is
-  // castling when the own king goes to a castling rook's square or
-  // (standard positions) to its two-square destination; everything else as
-  // written.  Nothing is checked here: verify() tests the move against the
-  // board before it (a code that names no move of the side to move fails
-  // there, at its own ply — and a failed ply ends the game's replay).
-  __device__ __forceinline__ static bool step(Scalars& b, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv) {
+  // One chain step (move j of the window): the move the code names, played on
+  // the lane bytes (lane l holds square l's piece code) and the scalars;
+  // returns it packed.  It is castling when the own king goes to a castling
+  // rook's square or (standard positions) to its two-square destination, with
+  // the rights of move j's board (Win); everything else as written.  Nothing
+  // is checked here: verify() tests the move against the board before it (a
+  // code that names no move of the side to move fails there, at its own ply —
+  // and a failed ply ends the game's replay).
+  __device__ __forceinline__ static bool step(Scalars& b, const Win& w, uint32_t j, uint32_t code, uint32_t& sqv,
+                                              int lane, uint32_t& mv) {
     const int from = (int)replay::tok_from(code), to = (int)replay::tok_to(code), promo = (int)replay::tok_piece(code);
     const int us = (int)b.stm;
     const uint32_t pc = replay::lane_value(sqv, from);
@@ -534,12 +588,13 @@ struct ChessRules {
     uint32_t v = sqv;
     int new_ep = -1;
     mv = (uint32_t)from | ((uint32_t)to << 6) | ((uint32_t)promo << 12);
-    if ((pc & 7) == KING) {  // castling, or a king move: the mover's rights go
+    if ((pc & 7) == KING) {  // castling, or a king move
       int rsq = -1;
       if (!promo) {
+        const uint32_t cr = rights(b.cr0, b.ksq, replay::lane_u64(w.pre, (int)j));
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-          const int r = sc_cr(b.cr, us, side);
+          const int r = sc_cr(cr, us, side);
           if (rsq < 0 && r >= 0 && (to == r || (!b.c960 && to == back + (side == 0 ? 6 : 2)))) rsq = r;
         }
       }
@@ -550,16 +605,9 @@ struct ChessRules {
         v = lane == kto ? pc : v;
         v = lane == rto ? (uint32_t)make_piece_d(us, ROOK) : v;
         mv = (uint32_t)from | ((uint32_t)rsq << 6) | (1u << 15);
-        b.cr |= 0xFFFFu << (16 * us);
       } else {
         v = lane == from ? 0u : v;
         v = lane == to ? (promo ? (uint32_t)make_piece_d(us, promo) : pc) : v;
-        b.cr |= 0xFFFFu << (16 * us);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t r = (b.cr >> (8 * i)) & 0xFFu;
-          if (r == (uint32_t)from || r == (uint32_t)to) b.cr |= 0xFFu << (8 * i);
-        }
       }
     } else {
       const bool pawn = (pc & 7) == PAWN;
@@ -567,13 +615,6 @@ struct ChessRules {
       v = (lane == from || lane == cap) ? 0u : v;
       v = lane == to ? (promo ? (uint32_t)make_piece_d(us, promo) : pc) : v;
       if (pawn && (from ^ to) == 16) new_ep = (from + to) >> 1;
-      if (cr_names(b.cr, (uint32_t)from) || cr_names(b.cr, (uint32_t)to)) {  // a castling rook moves or is taken
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t r = (b.cr >> (8 * i)) & 0xFFu;
-          if (r == (uint32_t)from || r == (uint32_t)to) b.cr |= 0xFFu << (8 * i);
-        }
-      }
     }
     sqv = v;
     b.ep = new_ep;

@@ -60,6 +60,9 @@ __device__ __forceinline__ void lds_fence() {
 
 // Lane `l`'s value of v, l wave-uniform (a scalar register read).
 __device__ __forceinline__ uint32_t lane_value(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
+  return (uint64_t)lane_value((uint32_t)v, l) | (uint64_t)lane_value((uint32_t)(v >> 32), l) << 32;
+}
 
 // v held in vector registers: the compiler treats a value read from one LDS
 // address by every lane as uniform and moves it to scalar registers, which
@@ -138,13 +141,18 @@ __device__ __forceinline__ void pack_nibbles(const uint32_t (&w)[16], uint32_t (
 //                                                       the standard start (< 64 characters) and its board
 //   uint32_t encode(const char* c, int len)             token -> code (kTokBad if malformed)
 //   Scalars scalars(const Board&); uint32_t lane_square(const Board&, int sq)
-//   bool step(Scalars&, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv)
-//                                                       one chain step: the move the code names, played on
-//                                                       the lane bytes; mv = that move packed (false: the
-//                                                       code names none, the replay stops there)
-//   kVary; void fix(Scalars&, const Scalars& s0, uint32_t plies)
-//                                                       the first kVary words change along the chain; fix
-//                                                       sets the rest from the window's first scalars
+//   Win window(const Scalars&, uint32_t code, uint32_t k, int lane)
+//                                                       lane-parallel per window (k moves, lane j's code):
+//                                                       what the chain and the checks derive scalars from
+//   bool step(Scalars&, const Win&, uint32_t j, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv)
+//                                                       one chain step (move j): the move the code names,
+//                                                       played on the lane bytes; mv = that move packed
+//                                                       (false: the code names none, the replay stops)
+//   kVary; void fix(Scalars&, const Scalars& s0, const Win&, uint32_t j, bool after)
+//                                                       the first kVary words change along the chain and
+//                                                       are collected; fix sets the rest for the board
+//                                                       before (after) move j
+//   void advance(Scalars&, const Win&, uint32_t k)      the scalars after the window's k moves
 //   Move unpack_move(uint32_t)
 //   Board board_from(const uint32_t (&w)[16], const Scalars&)   snapshot -> board (per lane)
 //   Pos pack_from(const uint32_t (&w)[16], const Scalars&)      snapshot -> record (per lane)
@@ -277,6 +285,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     // waits for nothing (its only LDS access is the snapshot byte store)
     asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(myc) : "memory");
     const Sc sc0 = sc;
+    const typename R::Win win = R::window(sc, myc, k, lane);
     uint32_t mvw = 0;
     uint32_t scw[R::kVary];
 #pragma unroll
@@ -285,7 +294,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     for (uint32_t j = 0; j < k; ++j) {
       const uint32_t code = lane_value(myc, (int)j);
       uint32_t mv;
-      if ((code & kTokBad) || !R::step(sc, code, sqv, lane, mv)) {
+      if ((code & kTokBad) || !R::step(sc, win, j, code, sqv, lane, mv)) {
         kplay = j;
         break;
       }
@@ -316,8 +325,8 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
         Sc before_sc, after_sc;
         __builtin_memcpy(&before_sc, sb, sizeof(Sc));
         __builtin_memcpy(&after_sc, sa, sizeof(Sc));
-        R::fix(before_sc, sc0, (uint32_t)lane);
-        R::fix(after_sc, sc0, (uint32_t)lane + 1);
+        R::fix(before_sc, sc0, win, (uint32_t)lane, false);
+        R::fix(after_sc, sc0, win, (uint32_t)lane, true);
         uint32_t wb[16], wa[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -339,6 +348,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
       bad_ply = done + first + 1;
       break;
     }
+    R::advance(sc, win, k);
     done += k;
     ntok -= k;
     // drop the consumed codes; the next window starts from the board after

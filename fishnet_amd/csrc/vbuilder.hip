@@ -49,8 +49,11 @@ struct VariantRules {
   // Along the chain the pockets, cr and ep change; stm alternates and the
   // variant word is fixed (the checking lanes derive those two).
   static constexpr int kVary = 6;
-  __device__ static void fix(Scalars& s, const Scalars& s0, uint32_t plies) {
-    s.stm = s0.stm ^ (plies & 1u);
+  struct Win {};
+  __device__ static Win window(const Scalars&, uint32_t, uint32_t, int) { return Win{}; }
+  __device__ static void advance(Scalars&, const Win&, uint32_t) {}
+  __device__ static void fix(Scalars& s, const Scalars& s0, const Win&, uint32_t j, bool after) {
+    s.stm = s0.stm ^ ((j + (after ? 1u : 0u)) & 1u);
     s.vc = s0.vc;
   }
   __device__ static Scalars scalars(const vb::VBoard& b) {
@@ -225,7 +228,8 @@ struct VariantRules {
   }
   // One chain step: interpret the code on the current board and play it;
   // false: it names no move of the side to move (the game's replay ends).
-  __device__ __forceinline__ static bool step(Scalars& b, uint32_t code, uint32_t& sqv, int lane, uint32_t& mv) {
+  __device__ __forceinline__ static bool step(Scalars& b, const Win&, uint32_t, uint32_t code, uint32_t& sqv, int lane,
+                                              uint32_t& mv) {
     vb::VMove m;
     if (!interpret(b, code, m, sqv)) return false;
     play(b, m, sqv, lane);

@@ -137,11 +137,11 @@ int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nba
 
 /* Where the last go() spent its time (diagnostics; the reference's engine
  * reports only time / nps per position).  Each net's games are cut into pieces
- * of about FNNUE_BACKEND_PIECE_PLIES plies (default 262144); a piece is one
+ * of about FNNUE_BACKEND_PIECE_PLIES plies (default 524288); a piece is one
  * host-to-device copy, the replay, the evaluation kernels and one device-to-
- * host copy of its results (plus the evaluator's error word).  The next
- * piece's copy and replay run beside this piece's evaluation, and the host
- * writes a piece's responses while the device works on the later ones. */
+ * host copy of its results (plus the evaluator's error word), in order on the
+ * net's stream; the host stages the next pieces and writes a piece's
+ * responses while the device works on the later ones. */
 typedef struct {
   double prep_ms;         /* host: sizes, move-work roots, text staging, copies and kernels enqueued */
   double device_ms;       /* host blocked waiting for the device */
