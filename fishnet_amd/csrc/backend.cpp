@@ -329,7 +329,9 @@ int variant_move_root(int variant, const fnnue_acquired& a, MoveRoot& R, std::ve
 // also carries the move-work children), staged as one image
 //   [text | fen_off | mv_off | ply_off | children | err (16 B) | fin | psqt | positional]
 // at its own place in the net's buffers: the first five parts and the zeroed
-// error word go up with one copy, the last four come back with one.
+// error words go up with one copy, the last four come back with one.  err
+// words 0-2 are the builder's (code, game, ply), word 3 the evaluator's: the
+// context's error word points there while the piece's evaluation is enqueued.
 struct Piece {
   std::vector<size_t> games;  // analysis batches (job indices)
   bool kids = false;          // the net's move-work children ride in this piece
@@ -360,7 +362,7 @@ struct NetWork {
   size_t next = 0;                // first piece whose responses are not written yet
   std::vector<hipEvent_t> ev_done;  // per piece: results and error word on the host
   DevBuf dev, pos;
-  PinnedBuf up, down, cerr;
+  PinnedBuf up, down;
   void clear() {
     games.clear();
     roots.clear();
@@ -386,7 +388,6 @@ struct NetWork {
     pos.release();
     up.release();
     down.release();
-    cerr.release();
     for (hipEvent_t e : ev_done) (void)hipEventDestroy(e);
     ev_done.clear();
   }
@@ -561,7 +562,6 @@ int fnnue_backend::plan(Job& j, int k) {
   if (int rc = W.dev.reserve(dev)) return rc;
   if (int rc = W.up.reserve(up)) return rc;
   if (int rc = W.down.reserve(down)) return rc;
-  if (int rc = W.cerr.reserve(4 * W.pieces.size())) return rc;
   if (pos)
     if (int rc = W.pos.reserve(pos)) return rc;
   return W.events(W.pieces.size());
@@ -614,8 +614,8 @@ int fnnue_backend::stage_up(Job& j, int k, size_t pi) {
 }
 
 // On the context's stream, behind the piece's replay: the CHAIN evaluation of
-// its plies, the children's evaluation, the results and the evaluator's error
-// word to the host.  Nothing waits.
+// its plies and the children's evaluation (latching into the piece's own
+// error word), then the results to the host.  Nothing waits.
 int fnnue_backend::stage_eval(int k, size_t pi) {
   NetWork& W = net[k];
   Piece& P = W.pieces[pi];
@@ -625,6 +625,12 @@ int fnnue_backend::stage_eval(int k, size_t pi) {
   char* dimg = W.dev.at<char>(P.dev0);
   int32_t* d_ps = reinterpret_cast<int32_t*>(dimg + P.o_ps);
   int32_t* d_po = reinterpret_cast<int32_t*>(dimg + P.o_po);
+  struct ErrWord {  // the context's error word, redirected for this piece's launches
+    fnnue_ctx* c;
+    uint32_t* saved;
+    ~ErrWord() { c->err = saved; }
+  } ew{c, c->err};
+  c->err = reinterpret_cast<uint32_t*>(dimg + P.o_res) + 3;
   if (P.ng) {
     const uint32_t* d_off = reinterpret_cast<const uint32_t*>(dimg + P.o_ply);
     const void* d_pos = W.pos.at<char>(P.pos0);
@@ -644,7 +650,6 @@ int fnnue_backend::stage_eval(int k, size_t pi) {
   }
   HIP_TRY(hipMemcpyAsync(W.down.at<char>(P.down0), dimg + P.o_res, P.end - P.o_res, hipMemcpyDeviceToHost, s),
           "D2H(results)");
-  HIP_TRY(hipMemcpyAsync(W.cerr.at<uint32_t>(4 * pi), c->err, 4, hipMemcpyDeviceToHost, s), "D2H(error word)");
   HIP_TRY(hipEventRecord(W.ev_done[pi], s), "hipEventRecord(results)");
   P.pending = true;
   mark("eval", k, (long)pi);
@@ -672,7 +677,8 @@ int fnnue_backend::finish(Job& j, int k, bool wait, bool* ready) {
   *ready = true;
   Piece& P = W.pieces[pi];
   P.pending = false;
-  if (W.down.at<uint32_t>(P.down0)[0] || *W.cerr.at<uint32_t>(4 * pi))
+  const uint32_t* err = W.down.at<uint32_t>(P.down0);
+  if (err[0] || err[3])
     if (int rc = recover(j, k, pi)) return rc;
   fill(j, k, P);
   ++W.next;
@@ -681,25 +687,14 @@ int fnnue_backend::finish(Job& j, int k, bool wait, bool* ready) {
 
 // A game the builder rejected (FEN / move), or whose positions the evaluator
 // rejects, fails its own batch: it is dropped from its piece and the piece is
-// staged again.  The evaluator's error word is sticky and shared by the net's
-// pieces, so the pieces already enqueued behind this one are staged again
-// after it is cleared.
+// staged again (its own error words: the other pieces are not affected).
 int fnnue_backend::recover(Job& j, int k, size_t pi) {
   NetWork& W = net[k];
-  fnnue_ctx* c = ctx[k];
-  hipStream_t s = c->stream;
   Piece& P = W.pieces[pi];
-  HIP_TRY(hipStreamSynchronize(s), "hipStreamSynchronize");
-  ++syncs;
-  // The drain also ran the evaluations enqueued behind this piece: whatever
-  // they latched is cleared here, and they are staged again below.
-  HIP_TRY(hipMemsetAsync(c->err, 0, 4, s), "hipMemsetAsync(error word)");
-  bool rebuilt = false;  // the error word was cleared before this piece's own first pass
   for (;;) {
     const uint32_t* berr = W.down.at<uint32_t>(P.down0);
-    const uint32_t cerr = *W.cerr.at<uint32_t>(4 * pi);
+    const uint32_t cerr = berr[3];
     if (!berr[0] && !cerr) break;
-    if (cerr && rebuilt) HIP_TRY(hipMemsetAsync(c->err, 0, 4, s), "hipMemsetAsync(error word)");
     if (berr[0]) {
       // The builder names the failing game; that batch fails (PositionFailed)
       // and the rest are staged again.  A count mismatch or a game index
@@ -740,7 +735,6 @@ int fnnue_backend::recover(Job& j, int k, size_t pi) {
       P.games.swap(keep);
     }
     ++rebuilds;
-    rebuilt = true;
     layout(j, k, P);  // fewer games: the piece still fits its place
     if (int rc = stage_up(j, k, pi)) return rc;
     if (int rc = stage_eval(k, pi)) return rc;
@@ -748,11 +742,6 @@ int fnnue_backend::recover(Job& j, int k, size_t pi) {
     ++syncs;
     P.pending = false;
   }
-  for (size_t q = pi + 1; q < W.pieces.size(); ++q)
-    if (W.pieces[q].pending) {
-      if (int rc = stage_up(j, k, q)) return rc;
-      if (int rc = stage_eval(k, q)) return rc;
-    }
   return FNNUE_OK;
 }
 
