@@ -14,20 +14,21 @@ rows = []
 for f in glob.glob(f"{d}/**/*hip_api_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-syncs = collections.Counter(r["Thread_Id"] for r in rows if r["Function"] == "hipStreamSynchronize")
+waits = ("hipStreamSynchronize", "hipEventSynchronize")
+syncs = collections.Counter(r["Thread_Id"] for r in rows if r["Function"] in waits)
 actor = syncs.most_common(1)[0][0]
 calls, cur, in_sync = [], [], False
 for r in rows:
     if r["Thread_Id"] != actor:
         continue
     f = r["Function"]
-    if f != "hipStreamSynchronize" and in_sync:
+    if f not in waits and in_sync and f in ("hipMemcpyAsync", "hipLaunchKernel"):
         calls.append(cur)
         cur = []
-    in_sync = f == "hipStreamSynchronize"
+    in_sync = f in waits if f not in ("hipEventQuery",) else in_sync
     cur.append(r)
 calls.append(cur)
-calls = [c for c in calls if any(r["Function"] == "hipStreamSynchronize" for r in c)]
+calls = [c for c in calls if any(r["Function"] in waits for r in c)]
 # each phase = warm-up calls + 1 probe + `per` timed calls; the timed ones are the last `per`
 n_phase = len(calls) // len(phases)
 alloc = ("hipMalloc", "hipFree", "hipHostMalloc", "hipHostFree", "hipMallocAsync", "hipFreeAsync")
