@@ -729,6 +729,19 @@ int eval_groups_device(fnnue_ctx* ctx, const void* d_pos, size_t pos_bytes, cons
   WorkspaceUse use{ctx, s};
   const bool sliced = ctx->ft_impl == FNNUE_FT_SLICED || ctx->variant != kVariantChess;
   if (sliced && ((rc = ensure_seg(ctx)) || (rc = ensure_span(ctx, npos)))) return rc;
+  if (sliced && npos <= seg_small_plan_max()) {
+    // a small call (a game or a few): spans, the offset check and the whole
+    // plan in one workgroup, then the main kernel and the stacks
+    std::array<hipEvent_t, 4>* ev = nullptr;
+    if ((rc = next_events(ctx, &ev)) || (rc = record_event(ctx, ev, 0, s))) return rc;
+    HIP_TRY(launch_seg_plan_small(ctx->variant, d_pos, (uint32_t)npos, d_off, (uint32_t)ngroups, ctx->seg.span, mode,
+                                  ctx->plan, ctx->seg, ctx->bucket, ctx->err, s),
+            "segment plan launch");
+    if ((rc = record_event(ctx, ev, 1, s))) return rc;
+    HIP_TRY(launch_seg_ft(ctx->hd, ctx->variant, (uint32_t)npos, mode, ctx->ptrs, ctx->plan, ctx->seg, ctx->x, s),
+            "ft_segments launch");
+    return run_chunk_tail(ctx, (uint32_t)npos, d_positional, s, ev, nullptr, ctx->plan.psqt_part, d_psqt);
+  }
   HIP_TRY(launch_group_span(d_off, (uint32_t)ngroups, (uint32_t)npos, sliced ? ctx->seg.span : nullptr, true,
                             ctx->err, s),
           "group_span launch");

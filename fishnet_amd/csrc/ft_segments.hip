@@ -172,12 +172,11 @@ struct SegCtr {
 // is written by the first kernel (by its small group, or as a big group's
 // marker), so the second kernel never reads a stale entry.
 constexpr uint32_t kSpanChunk = 4096;
-__global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
-                                                         uint32_t npos, uint2* __restrict__ span, int check,
-                                                         uint32_t* __restrict__ err) {
-  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= ngroups) return;
-  if (check && (threadIdx.x & 63) == 0) {
+// group g's span entries, by one wave (lane)
+__device__ __forceinline__ void group_span_one(const uint32_t* __restrict__ off, uint32_t ngroups, uint32_t npos,
+                                               uint2* __restrict__ span, int check, uint32_t* __restrict__ err,
+                                               uint32_t g, uint32_t lane) {
+  if (check && lane == 0) {
     bool bad = off[g + 1] < off[g];
     if (g == 0) bad |= off[0] != 0 || off[ngroups] != npos;
     if (bad) atomicOr(err, 2u);
@@ -185,7 +184,6 @@ __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restr
   if (!span) return;
   const uint32_t a = min(off[g], npos), b = min(max(off[g + 1], a), npos);
   const uint2 v = make_uint2(a, b);
-  const uint32_t lane = threadIdx.x & 63;
   if (b - a <= kSpanChunk) {
     for (uint32_t i = a + lane; i < b; i += 64) span[i] = v;
     return;
@@ -193,6 +191,14 @@ __global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restr
   const uint32_t a1 = (a + kSpanChunk - 1) / kSpanChunk * kSpanChunk;  // < b: the group is longer than a chunk
   for (uint32_t i = a + lane; i < a1; i += 64) span[i] = v;
   for (uint32_t i = a1 + lane * kSpanChunk; i < b; i += 64 * kSpanChunk) span[i] = v;
+}
+
+__global__ __launch_bounds__(256) void group_span_kernel(const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                         uint32_t npos, uint2* __restrict__ span, int check,
+                                                         uint32_t* __restrict__ err) {
+  const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  group_span_one(off, ngroups, npos, span, check, err, g, threadIdx.x & 63);
 }
 
 __global__ __launch_bounds__(256) void group_span_big_kernel(uint32_t npos, uint2* __restrict__ span) {
@@ -433,25 +439,24 @@ __global__ __launch_bounds__(256) void seg_items_scan_kernel(uint32_t n, const u
 //   segment's records are contiguous.
 // At most one workgroup per CU: the histogram merge costs one global atomic
 // per non-empty bin per workgroup.
+// (The body runs as workgroup `bid` of `nb`, on an LDS histogram h of
+// SegCtr<Fs>::kIB words: seg_place_kernel, or a phase of seg_plan_small_kernel.)
 template <class Fs>
-__global__ __launch_bounds__(1024) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, uint32_t sbase,
-                                                         int star,
-                                                         const uint8_t* __restrict__ bucket,
-                                                         const uint32_t* __restrict__ ref,
-                                                         const uint32_t* __restrict__ cref,
-                                                         const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len,
-                                                         const uint4* __restrict__ dtmp, uint4* __restrict__ drec,
-                                                         uint32_t* __restrict__ ctr) {
+__device__ __forceinline__ void seg_place_body(uint32_t n, const uint2* __restrict__ span, uint32_t sbase, int star,
+                                               const uint8_t* __restrict__ bucket, const uint32_t* __restrict__ ref,
+                                               const uint32_t* __restrict__ cref, const uint32_t* __restrict__ ipos,
+                                               uint32_t* __restrict__ len, const uint4* __restrict__ dtmp,
+                                               uint4* __restrict__ drec, uint32_t* __restrict__ ctr,
+                                               uint32_t* __restrict__ h, uint32_t bid, uint32_t nb) {
   constexpr int kIB = SegCtr<Fs>::kIB;
-  __shared__ uint32_t h[kIB];
   for (int t = threadIdx.x; t < kIB; t += blockDim.x) h[t] = 0;
   __syncthreads();
   // Record 2n, read by items past the end of their segment: no rows, x row 2n
   // and bucket 0, i.e. x and PSQT stores just past the launch's buffer ranges
   // (dropped by the hardware), so the walk needs no liveness masking.
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+  if (bid == 0 && threadIdx.x == 0)
     drec[2 * n] = make_uint4(2 * n, Fs::kNone | Fs::kNone << 16, Fs::kNone | Fs::kNone << 16, 0u);
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < 2 * n; j += gridDim.x * blockDim.x) {
+  for (uint32_t j = bid * blockDim.x + threadIdx.x; j < 2 * n; j += nb * blockDim.x) {
     const uint32_t c = j >= n ? 1u : 0u, i = j - c * n;
     const uint32_t rf = ref[j];
     if (rf) {
@@ -486,6 +491,19 @@ __global__ __launch_bounds__(1024) void seg_place_kernel(uint32_t n, const uint2
 }
 
 template <class Fs>
+__global__ __launch_bounds__(1024) void seg_place_kernel(uint32_t n, const uint2* __restrict__ span, uint32_t sbase,
+                                                         int star,
+                                                         const uint8_t* __restrict__ bucket,
+                                                         const uint32_t* __restrict__ ref,
+                                                         const uint32_t* __restrict__ cref,
+                                                         const uint32_t* __restrict__ ipos, uint32_t* __restrict__ len,
+                                                         const uint4* __restrict__ dtmp, uint4* __restrict__ drec,
+                                                         uint32_t* __restrict__ ctr) {
+  __shared__ uint32_t h[SegCtr<Fs>::kIB];
+  seg_place_body<Fs>(n, span, sbase, star, bucket, ref, cref, ipos, len, dtmp, drec, ctr, h, blockIdx.x, gridDim.x);
+}
+
+template <class Fs>
 __device__ __forceinline__ uint32_t seg_key(const typename Fs::Dec& d, int c, uint32_t L) {
   return (uint32_t)Fs::block(c, c ? d.b.bk : d.b.wk) * SegCtr<Fs>::kNB + seg_len_bin(L) * Fs::kClasses +
          seg_count_class<Fs::kClasses>((uint32_t)d.nfeat);
@@ -495,21 +513,20 @@ __device__ __forceinline__ uint32_t seg_key(const typename Fs::Dec& d, int c, ui
 // perspective k >= cref[n]); invalid positions are refreshes with len 0.
 // Sorted item record: {root | half << 24 | bucket << 25, length, perspective,
 // list length + 1}; full feature list of the root as in the sliced plan.
+// (As workgroup bid of nb on LDS lcnt / lbase of SegCtr<Fs>::kIB words and
+// lists of 1024 * kListStrideWords words.)
 template <class Fs>
-__global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
-                                                           const uint32_t* __restrict__ cref,
-                                                           const uint32_t* __restrict__ ipos,
-                                                           const uint32_t* __restrict__ len,
-                                                           uint32_t* __restrict__ ctr, uint4* __restrict__ items,
-                                                           uint16_t* __restrict__ flist) {
+__device__ __forceinline__ void seg_scatter_body(const typename Fs::Pos* __restrict__ pos, uint32_t n,
+                                                 const uint32_t* __restrict__ cref, const uint32_t* __restrict__ ipos,
+                                                 const uint32_t* __restrict__ len, uint32_t* __restrict__ ctr,
+                                                 uint4* __restrict__ items, uint16_t* __restrict__ flist,
+                                                 uint32_t* __restrict__ lcnt, uint32_t* __restrict__ lbase,
+                                                 uint32_t* __restrict__ lists, uint32_t bid, uint32_t nb) {
   constexpr int kIB = SegCtr<Fs>::kIB;
-  __shared__ uint32_t lcnt[kIB];
-  __shared__ uint32_t lbase[kIB];
-  __shared__ uint32_t lists[1024 * kListStrideWords];  // list staging, one row per lane
   const uint32_t K = cref[2 * n], K0 = cref[n];
   // Grid-stride over 1024-item blocks: the item count is known only here, and
   // a grid sized for 2n items launched mostly empty 103-KB workgroups.
-  for (uint32_t b0 = blockIdx.x * blockDim.x; b0 < K; b0 += gridDim.x * blockDim.x) {
+  for (uint32_t b0 = bid * blockDim.x; b0 < K; b0 += nb * blockDim.x) {
     __syncthreads();  // the previous block's LDS counts are read
     for (int i = threadIdx.x; i < kIB; i += blockDim.x) lcnt[i] = 0;
     __syncthreads();
@@ -536,6 +553,108 @@ __global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Po
       Fs::write_list(d, (int)c, slot, pp, lists + threadIdx.x * kListStrideWords, flist);
     }
   }
+}
+
+template <class Fs>
+__global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
+                                                           const uint32_t* __restrict__ cref,
+                                                           const uint32_t* __restrict__ ipos,
+                                                           const uint32_t* __restrict__ len,
+                                                           uint32_t* __restrict__ ctr, uint4* __restrict__ items,
+                                                           uint16_t* __restrict__ flist) {
+  constexpr int kIB = SegCtr<Fs>::kIB;
+  __shared__ uint32_t lcnt[kIB];
+  __shared__ uint32_t lbase[kIB];
+  __shared__ uint32_t lists[1024 * kListStrideWords];  // list staging, one row per lane
+  seg_scatter_body<Fs>(pos, n, cref, ipos, len, ctr, items, flist, lcnt, lbase, lists, blockIdx.x, gridDim.x);
+}
+
+// The whole plan of a small grouped call (npos <= kSegSmallPlan, one chunk)
+// in ONE workgroup: group spans (and the offset check), deltas, the scan of
+// refresh flags, segment placement, the unit table and the sorted items with
+// their lists — the phases of group_span .. seg_scatter, separated by
+// workgroup barriers instead of kernel boundaries (for a game or a few, each
+// of those eight launches is mostly its launch-to-launch gap: ~45 µs in all,
+// profiles/r05/backend/timeline_1batch.txt).  Global memory written by one
+// phase is read by the next from the same CU, ordered by the barrier.
+constexpr uint32_t kSegSmallPlan = 8192;
+template <class Fs>
+constexpr int seg_small_lds_words() {
+  constexpr int kIB = SegCtr<Fs>::kIB;
+  constexpr int scatter = 2 * kIB + 1024 * kListStrideWords;
+  constexpr int scan = plan_scan_lds_words<Fs::KB, SegCtr<Fs>::kNB>();
+  return scatter > scan ? scatter : scan;
+}
+template <class Fs>
+__global__ __launch_bounds__(1024) void seg_plan_small_kernel(const typename Fs::Pos* __restrict__ pos, uint32_t n,
+                                                              const uint32_t* __restrict__ off, uint32_t ngroups,
+                                                              uint2* __restrict__ span, int star,
+                                                              uint32_t* __restrict__ ref, uint4* __restrict__ dtmp,
+                                                              uint8_t* __restrict__ bucket, uint32_t* __restrict__ err,
+                                                              uint32_t* __restrict__ cref, uint32_t* __restrict__ ipos,
+                                                              uint32_t* __restrict__ len, uint4* __restrict__ drec,
+                                                              uint32_t* __restrict__ ctr, int4* __restrict__ units,
+                                                              uint32_t seg_plies, uint4* __restrict__ items,
+                                                              uint16_t* __restrict__ flist) {
+  constexpr int kIB = SegCtr<Fs>::kIB;
+  __shared__ uint32_t lds[seg_small_lds_words<Fs>()];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // counters, then each group's span entries (one wave per group) and the
+  // offset check; a group longer than kSpanChunk: its chunks' entries after
+  for (uint32_t k = t; k < (uint32_t)SegCtr<Fs>::kWords; k += 1024) ctr[k] = 0;
+  for (uint32_t g = wv; g < ngroups; g += 16) group_span_one(off, ngroups, n, span, 1, err, g, lane);
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < n; c0 += kSpanChunk) {
+    const uint2 v = span[c0];
+    if (v.y - v.x <= kSpanChunk) continue;
+    const uint32_t e = min(c0 + kSpanChunk, min(v.y, n));
+    for (uint32_t i = c0 + 1 + t; i < e; i += 1024) span[i] = v;
+  }
+  __syncthreads();
+  // deltas and refresh flags, 1024 positions at a time (their decodes shared
+  // through LDS as seg_delta_kernel's block of 256 does)
+  for (uint32_t i0 = 0; i0 < n; i0 += 1024) {
+    const uint32_t i = i0 + t;
+    typename Fs::Dec B;
+    B.ok = B.over = false;
+    B.b.wk = B.b.bk = 0;
+    if (i < n) B = Fs::template decode<false>(pos + i);
+    lds[t] = seg_info(B);
+    __syncthreads();
+    uint32_t r0 = 0, r1 = 0;
+    if (i < n) seg_delta_one<Fs>(pos, n, span, 0u, star, ref, dtmp, bucket, err, i, i0, lds, B, r0, r1);
+    __syncthreads();
+  }
+  // cref = exclusive scan of the refresh flags over both perspectives (2n),
+  // ipos[k] = the position of item k, cref[2n] = the item count
+  uint32_t base = 0;
+  for (uint32_t j0 = 0; j0 < 2 * n; j0 += 1024) {
+    const uint32_t j = j0 + t;
+    const uint32_t r = j < 2 * n ? ref[j] : 0u;
+    const uint64_t bal = __ballot(r != 0);
+    if (lane == 0) lds[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t below = (uint32_t)__popcll(bal & ((1ull << lane) - 1)), tot = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      const uint32_t c = lds[w];
+      below += w < wv ? c : 0u;
+      tot += c;
+    }
+    if (j < 2 * n) {
+      const uint32_t k = base + below;
+      cref[j] = k;
+      if (r) ipos[k] = j >= n ? j - n : j;
+    }
+    base += tot;
+    __syncthreads();
+  }
+  if (t == 0) cref[2 * n] = base;
+  __syncthreads();
+  seg_place_body<Fs>(n, span, 0u, star, bucket, ref, cref, ipos, len, dtmp, drec, ctr, lds, 0u, 1u);
+  __syncthreads();
+  plan_scan_body<Fs::KB, SegCtr<Fs>::kNB>(ctr, units, 0u, seg_plies, nullptr, lds);
+  __syncthreads();
+  seg_scatter_body<Fs>(pos, n, cref, ipos, len, ctr, items, flist, lds, lds + kIB, lds + 2 * kIB, 0u, 1u);
 }
 
 struct SegFetch {
@@ -993,6 +1112,25 @@ hipError_t launch_seg_plan(int variant, const void* pos, uint32_t n, const void*
     return seg_plan_t<VariantFs<kVariantCrazyhouse>>(vp, n, sp, sbase, star, P, G, bucket, err, stream);
   if (variant == kVariantAtomic)
     return seg_plan_t<VariantFs<kVariantAtomic>>(vp, n, sp, sbase, star, P, G, bucket, err, stream);
+  return hipErrorInvalidValue;
+}
+
+uint32_t seg_small_plan_max() { return kSegSmallPlan; }
+
+hipError_t launch_seg_plan_small(int variant, const void* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
+                                 void* span, int mode, const SlicedPlan& P, const SegPlan& G, uint8_t* bucket,
+                                 uint32_t* err, hipStream_t stream) {
+  if (n == 0 || n > kSegSmallPlan) return hipErrorInvalidValue;
+  const int star = mode == FNNUE_GROUP_STAR ? 1 : 0;
+#define FNNUE_SMALL_PLAN(Fs, P_T)                                                                                  \
+  hipLaunchKernelGGL(seg_plan_small_kernel<Fs>, dim3(1), dim3(1024), 0, stream, static_cast<const P_T*>(pos), n, off, \
+                     ngroups, static_cast<uint2*>(span), star, G.ref, (uint4*)G.dtmp, bucket, err, G.cref, G.ipos,  \
+                     G.len, (uint4*)G.drec, P.ctr, (int4*)P.units, G.unit_plies, (uint4*)G.items, P.flist);        \
+  return hipGetLastError();
+  if (variant == kVariantChess) { FNNUE_SMALL_PLAN(ChessFs, fnnue_pos) }
+  if (variant == kVariantCrazyhouse) { FNNUE_SMALL_PLAN(VariantFs<kVariantCrazyhouse>, fnnue_vpos) }
+  if (variant == kVariantAtomic) { FNNUE_SMALL_PLAN(VariantFs<kVariantAtomic>, fnnue_vpos) }
+#undef FNNUE_SMALL_PLAN
   return hipErrorInvalidValue;
 }
 

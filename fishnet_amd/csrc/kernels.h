@@ -134,6 +134,13 @@ hipError_t launch_ft_segments(uint32_t hd, int variant, const void* pos, uint32_
 // feature set only, not on the net: a second net of the same feature set (the
 // small net beside the big one) runs its main kernel over the same plan
 // (P.ctr / units / flist and G), with its own tiles, swar flag, psqt_part, x.
+// A grouped call of at most seg_small_plan_max() positions: spans, offset
+// check and the whole plan of its one chunk in one workgroup (then
+// launch_seg_ft).
+uint32_t seg_small_plan_max();
+hipError_t launch_seg_plan_small(int variant, const void* pos, uint32_t n, const uint32_t* off, uint32_t ngroups,
+                                 void* span, int mode, const SlicedPlan& P, const SegPlan& G, uint8_t* bucket,
+                                 uint32_t* err, hipStream_t stream);
 hipError_t launch_seg_plan(int variant, const void* pos, uint32_t n, const void* span, uint32_t sbase, int mode,
                            const SlicedPlan& P, const SegPlan& G, uint8_t* bucket, uint32_t* err, hipStream_t stream);
 // A second unit table over a chunk's plan (after launch_seg_plan): units of

@@ -207,16 +207,21 @@ __host__ __device__ constexpr uint32_t seg_count_class(uint32_t nfeat) {
 // position bins, then offsets, cursors and the unit count (kCnt / kOff / kCur
 // / kNUnits for KB = 32, kV* for 64, SegCtr for segments).  NB = 33: bin =
 // list length (fixed-size units); NB = 33 C: bin = C * length bin + class.
+// The body runs in any 1024-thread workgroup (plan_scan_kernel_t, or a phase of
+// the one-workgroup segment plan) on LDS the caller provides:
+// plan_scan_lds_words<KB, NB>() words.
+template <int KB, int NB>
+__host__ __device__ constexpr int plan_scan_lds_words() {
+  return (KB * NB + kPosBins) + 16 + KB * NB + KB + 1;
+}
 template <int KB, int NB = 33>
-__global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel_t(uint32_t* __restrict__ ctr,
-                                                                                  int4* __restrict__ units,
-                                                                                  uint32_t unit_items,
-                                                                                  uint32_t seg_plies = 0,
-                                                                                  uint32_t* __restrict__ nu_out = nullptr) {
+__device__ __forceinline__ void plan_scan_body(uint32_t* __restrict__ ctr, int4* __restrict__ units,
+                                               uint32_t unit_items, uint32_t seg_plies, uint32_t* __restrict__ nu_out,
+                                               uint32_t* __restrict__ lds) {
   constexpr int kIB = KB * NB, kB = kIB + kPosBins, kO = kB, kC = 2 * kB, kNU = 3 * kB;
   auto len_bin = [](int i) { return (i % NB) / (NB / 33); };
-  __shared__ uint32_t s[kB];
-  __shared__ uint32_t part[16];
+  uint32_t* s = lds;             // [kB]
+  uint32_t* part = lds + kB;     // [16]
   const int t = threadIdx.x;
   // Exclusive scan of the item bins and, separately, of the position bins.
   constexpr int per = (kB + 1023) / 1024;
@@ -267,8 +272,8 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     // cumulative work (a bin's items weighed seg_bin_weight) reaches
     // u * seg_plies.  Bins are contiguous in item order, so each
     // (kb, bin) thread places the unit starts falling inside its bin.
-    __shared__ uint32_t pb[kIB];        // positions before bin i within its king block
-    __shared__ uint32_t ubase[KB + 1];  // first unit of each king block
+    uint32_t* pb = lds + kB + 16;           // [kIB] positions before bin i within its king block
+    uint32_t* ubase = lds + kB + 16 + kIB;  // [KB + 1] first unit of each king block
     for (int k = 0; k < per; ++k) {     // local[k] = count of bin t*per + k
       const int i = t * per + k;
       if (i < kIB) pb[i] = local[k] * seg_bin_weight(len_bin(i));
@@ -329,6 +334,16 @@ __global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel
     for (uint32_t c = b; c < e; c += unit_items) units[nu++] = make_int4(kb, (int)c, (int)min(e, c + unit_items), 0);
     if (kb == KB - 1) ctr[kNU] = incl;
   }
+}
+
+template <int KB, int NB = 33>
+__global__ __launch_bounds__(1024) __attribute__((unused)) void plan_scan_kernel_t(uint32_t* __restrict__ ctr,
+                                                                                  int4* __restrict__ units,
+                                                                                  uint32_t unit_items,
+                                                                                  uint32_t seg_plies = 0,
+                                                                                  uint32_t* __restrict__ nu_out = nullptr) {
+  __shared__ uint32_t lds[plan_scan_lds_words<KB, NB>()];
+  plan_scan_body<KB, NB>(ctr, units, unit_items, seg_plies, nu_out, lds);
 }
 
 constexpr int kListStrideWords = 17;  // words per lane of the list staging rows (68 B)
