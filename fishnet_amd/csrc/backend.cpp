@@ -3,9 +3,10 @@
 //   stockfish::channel -> (StockfishStub, StockfishActor)   [ref] src/stockfish.rs:23-61
 // is a bounded mpsc channel (capacity 1) into an actor owning one engine
 // process; StockfishStub::go sends a Position with a oneshot callback and
-// maps any failure to PositionFailed{batch_id}.  Here the actor is a worker
-// thread owning one fnnue_ctx per net (chess, and optionally the crazyhouse
-// and atomic variant nets); a message carries whole acquired batches
+// maps any failure to PositionFailed{batch_id}.  Here the actor owns one
+// fnnue_ctx per net (chess, and optionally the crazyhouse and atomic variant
+// nets) and answers one message at a time on the caller's thread (a second
+// caller waits: the capacity-1 channel); a message carries whole acquired batches
 // (AcquireResponseBody, [ref] src/api.rs:293-309), expanded the way
 // IncomingBatch::from_acquired does ([ref] src/queue.rs:518-627) — but on the
 // device: the FEN/UCI text goes to HBM once, the builder replays every game
@@ -56,7 +57,7 @@ using Clock = std::chrono::steady_clock;
 
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
 
-// One message on the channel: StockfishMessage::Go with its callback.
+// One message on the channel: StockfishMessage::Go with its answer.
 struct Job {
   const fnnue_acquired* batches = nullptr;
   size_t nb = 0;
@@ -65,8 +66,7 @@ struct Job {
   uint32_t* off = nullptr;
   int32_t* rc = nullptr;
   int ret = 0;
-  std::string err;  // the actor thread's fnnue_last_error, handed to the caller
-  bool done = false;
+  std::string err;  // fnnue_last_error of a failed call
 };
 
 // Grow-only device buffer.
@@ -402,11 +402,12 @@ struct fnnue_backend {
   int device = 0;
   int32_t norm = kNormalizeToPawnSf151;
   size_t piece_plies = 524288;  // FNNUE_BACKEND_PIECE_PLIES
-  std::thread th;
-  std::mutex mu;
-  std::condition_variable cv;  // slot / done / stop changes
-  Job* slot = nullptr;         // the capacity-1 channel
-  bool stop = false;
+  // The capacity-1 channel: a go() runs on its caller's thread holding run_mu,
+  // so a second caller waits until the first call is answered
+  // (mpsc::channel(1) with one message in flight, without a thread hand-off
+  // each way: ~10 µs of a one-batch call).
+  std::mutex run_mu;
+  bool closed = false;
   Workers pool;
   int pool_threads = 1;
   NetWork net[kKinds];
@@ -442,22 +443,6 @@ struct fnnue_backend {
   int recover(Job& j, int k, size_t pi);
   void fill(Job& j, int k, const Piece& P);
   void fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint32_t nps);
-  void loop() {
-    std::unique_lock<std::mutex> lk(mu);
-    for (;;) {
-      cv.wait(lk, [&] { return slot != nullptr || stop; });
-      if (!slot) return;  // stop with an empty channel
-      Job* j = slot;
-      slot = nullptr;
-      cv.notify_all();  // the channel has room again
-      lk.unlock();
-      g_err.clear();
-      run(*j);
-      lk.lock();
-      j->done = true;
-      cv.notify_all();
-    }
-  }
 };
 
 // Move batches of one net, host side: the position after all moves (one per
@@ -1070,15 +1055,11 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
   }
   try {
     b->pool.start(b->pool_threads);
-    b->th = std::thread([b] {
-      DeviceGuard g(b->device);
-      b->loop();
-    });
   } catch (const std::system_error&) {
     b->pool.stop();
     for (fnnue_ctx* c : b->ctx) fnnue_ctx_free(c);
     delete b;
-    return fail(FNNUE_E_OOM, "could not start the actor thread");
+    return fail(FNNUE_E_OOM, "could not start the host worker threads");
   }
   *out = b;
   return FNNUE_OK;
@@ -1098,11 +1079,9 @@ int fnnue_backend_channel(const fnnue_net* net, int device, const fnnue_backend_
 void fnnue_backend_free(fnnue_backend* b) {
   if (!b) return;
   {
-    std::lock_guard<std::mutex> lk(b->mu);
-    b->stop = true;
+    std::lock_guard<std::mutex> lk(b->run_mu);  // after the call in flight
+    b->closed = true;
   }
-  b->cv.notify_all();
-  if (b->th.joinable()) b->th.join();
   b->pool.stop();
   {
     DeviceGuard g(b->device);
@@ -1123,13 +1102,11 @@ int fnnue_backend_go(fnnue_backend* b, const fnnue_acquired* batches, size_t nba
   j.cap = cap;
   j.off = off;
   j.rc = batch_rc;
-  std::unique_lock<std::mutex> lk(b->mu);
-  b->cv.wait(lk, [&] { return b->slot == nullptr || b->stop; });  // mpsc::Sender::send on a full channel
-  if (b->stop) return fail(FNNUE_E_DEVICE, "backend actor stopped");
-  b->slot = &j;
-  b->cv.notify_all();
-  b->cv.wait(lk, [&] { return j.done; });  // the oneshot callback
-  lk.unlock();
+  std::lock_guard<std::mutex> lk(b->run_mu);  // mpsc::Sender::send on a full channel waits
+  if (b->closed) return fail(FNNUE_E_DEVICE, "backend actor stopped");
+  DeviceGuard g(b->device);
+  g_err.clear();
+  b->run(j);
   if (j.ret) return fail(j.ret, j.err);
   return FNNUE_OK;
 }

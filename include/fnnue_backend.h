@@ -12,10 +12,11 @@
  * (src/queue.rs:518-627) from an AcquireResponseBody (src/api.rs:293-309).
  *
  * Here the same pair is a channel to one evaluator per net on one GPU: the
- * actor is a worker thread owning an fnnue_ctx per net (chess, and optionally
- * the crazyhouse and atomic Fairy-Stockfish variant nets); a go() sends it
- * whole acquired batches (capacity-1 channel: a second caller waits, as on
- * the reference's mpsc::channel(1)) and returns one response per position.
+ * actor owns an fnnue_ctx per net (chess, and optionally the crazyhouse and
+ * atomic Fairy-Stockfish variant nets); a go() hands it whole acquired
+ * batches, which it answers on the calling thread, one call at a time (a
+ * second caller waits, as on the reference's mpsc::channel(1)), returning
+ * one response per position.
  * Each batch goes to the net of its variant (the reference picks the engine
  * by EngineFlavor, src/queue.rs:530-539, and the variant, src/assets.rs:
  * 384-391).  The expansion (FEN parse, UCI replay, every ply) runs on the
@@ -113,9 +114,10 @@ typedef struct {
   const fnnue_net *atomic;     /* a FNNUE_VARIANT_ATOMIC net */
 } fnnue_backend_nets;
 
-/* stockfish::channel: starts the actor (worker thread + one evaluator per net
- * on `device`).  A net in the wrong slot: FNNUE_E_ARCH.  init may be NULL
- * (defaults).  The nets may be freed after the call. */
+/* stockfish::channel: starts the actor (one evaluator per net on `device`, a
+ * few host threads for the per-batch loops of large calls).  A net in the
+ * wrong slot: FNNUE_E_ARCH.  init may be NULL (defaults).  The nets may be
+ * freed after the call. */
 int fnnue_backend_channel_nets(const fnnue_backend_nets *nets, int device, const fnnue_backend_init *init,
                                fnnue_backend **out);
 /* The one-net form: the net goes to the slot of its variant. */
