@@ -798,10 +798,8 @@ namespace {
 hipError_t launch_chess_replay(const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                const uint32_t* d_ply_off, uint32_t ngames, fnnue_pos* d_out, DBoard* d_states,
                                uint8_t* d_final, uint32_t* d_err, hipStream_t s) {
-  if (!ngames) return hipSuccess;
-  hipLaunchKernelGGL(replay::replay_wave_kernel<ChessRules>, dim3(ngames), dim3(64), 0, s, (int)kVariantChess, d_text,
-                     d_fen_off, d_mv_off, ngames, d_ply_off, d_out, d_states, d_err, d_final);
-  return hipGetLastError();
+  return replay::launch_replay<ChessRules>((int)kVariantChess, d_text, d_fen_off, d_mv_off, ngames, d_ply_off, d_out,
+                                           d_states, d_err, d_final, s);
 }
 
 }  // namespace

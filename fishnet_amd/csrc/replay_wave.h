@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "builder.h"
 
@@ -160,6 +161,207 @@ __device__ __forceinline__ void pack_nibbles(const uint32_t (&w)[16], uint32_t (
 //   Pos pack(const Board&)
 //   bool any_legal_from(const Board&, int sq, bool drops) legal moves of the piece on sq (+ drops)
 //   uint8_t end_flags(const Board&, bool any)             kFinal* of a last position
+// ---- phases, shared by the one-wave and the two-wave kernel ----
+
+// The root: the FEN through LDS (TXT), parsed by every lane alike.  One longer
+// than kTxt characters (a legal FEN has < 100) is rejected as unparsable.
+template <class R>
+__device__ __forceinline__ bool root_board(int variant, const char* __restrict__ text, uint32_t f0, uint32_t m0,
+                                           char* TXT, int lane, typename R::Board& root) {
+  const uint32_t flen = m0 - f0;
+  if (flen > (uint32_t)kTxt) return false;
+  for (uint32_t i = lane; i < flen; i += 64) TXT[i] = text[f0 + i];
+  lds_fence();
+  // Most games start from the variant's standard position: recognised by one
+  // lane-parallel compare, its board is a constant (the parser's own result,
+  // tests/test_gpu_builder.py); any other FEN is parsed.
+  const char* sf = R::start_fen(variant);
+  const uint32_t sl = R::start_fen_len(variant);
+  const bool same = flen == sl && __ballot((uint32_t)lane < sl && TXT[lane] != sf[lane]) == 0;
+  if (same) {
+    root = R::start_board(variant);
+    return true;
+  }
+  return R::parse_fen(TXT, 0, flen, variant, root);
+}
+
+// The tokeniser's place in the game's move text [p, e): TXT holds the text
+// from tbase on (kTxt characters at a time, ' ' past the end), TK[0, ntok) the
+// pending codes.
+struct Tok {
+  uint32_t p, tbase, ntok;
+  bool staged;
+  char prev;  // the character before p
+};
+
+// Tokenise 64 characters at a time (lane = character: token starts by
+// ballot, each starting lane encodes its token) until `need` codes are
+// pending or the text ends.
+template <class R>
+__device__ __forceinline__ void tokenise(Tok& t, const char* __restrict__ text, uint32_t e, char* TXT, uint32_t* TK,
+                                         uint32_t need, int lane) {
+  while (t.ntok < need && t.p < e) {
+    if (!t.staged || t.p + 64 + 6 > t.tbase + (uint32_t)kTxt) {
+      t.tbase = t.p;
+      t.staged = true;
+      const uint32_t lim = min((uint32_t)kTxt, e - t.tbase + 72);  // the text, then spaces for any token tail
+      for (uint32_t q = lane; q < lim; q += 64) TXT[q] = t.tbase + q < e ? text[t.tbase + q] : ' ';
+      lds_fence();
+    }
+    const uint32_t i = t.p - t.tbase + lane;
+    const char c = TXT[i];
+    const char cprev = (char)__shfl_up((int)c, 1, 64);
+    const bool start = !space(c) && space(lane == 0 ? t.prev : cprev);
+    const uint64_t starts = __ballot(start);
+    if (start) {
+      char w[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) w[q] = TXT[i + q];
+      int len = 1;
+      bool more = true;
+#pragma unroll
+      for (int q = 1; q < 6; ++q) {
+        more = more && !space(w[q]);
+        len += more ? 1 : 0;
+      }
+      const uint32_t code = (len == 4 || len == 5) ? R::encode(w, len) : kTokBad;
+      const uint32_t idx = t.ntok + (uint32_t)__popcll(starts & ((1ull << lane) - 1));
+      if (idx < (uint32_t)kTokRing) TK[idx] = code;
+    }
+    t.ntok += (uint32_t)__popcll(starts);
+    t.prev = (char)__shfl((int)c, 63, 64);
+    t.p += 64;
+  }
+  lds_fence();
+}
+
+// Drops the k codes a window took from the ring.
+__device__ __forceinline__ void tok_consume(Tok& t, uint32_t* TK, uint32_t k, int lane) {
+  t.ntok -= k;
+  uint32_t keep[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const uint32_t src = k + lane + 64 * r;
+    keep[r] = src < (uint32_t)kTokRing ? TK[src] : 0;
+  }
+  lds_fence();
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+    if ((uint32_t)lane + 64 * r < t.ntok) TK[lane + 64 * r] = keep[r];
+  lds_fence();
+}
+
+// After the game's last code: is there text left that holds another token?
+__device__ __forceinline__ bool tok_extra(Tok& t, const char* __restrict__ text, uint32_t e, int lane) {
+  bool extra = t.ntok != 0;
+  for (uint32_t q = t.p; q < e && !extra; q += 64) {
+    const uint32_t i = q + lane;
+    const char c = i < e ? text[i] : ' ';
+    const char cprev = (char)__shfl_up((int)c, 1, 64);
+    extra = __ballot(!space(c) && space(lane == 0 ? t.prev : cprev)) != 0;
+    t.prev = (char)__shfl((int)c, 63, 64);
+  }
+  return extra;
+}
+
+// The chain, wave-uniform: interpret and play the window's k moves (lane j's
+// code myc is move j).  The board is lane bytes — lane l holds square l's
+// piece (sqv), so a move is a handful of lane-parallel selects — plus the
+// wave-uniform scalars.  SNAP[0] gets the window's first board, SNAP[j + 1]
+// the board after move j; lane j collects move j packed (mvw) and the kVary
+// scalar words after it (scw).  Returns the moves played (< k: a code that
+// names no move; that ply fails its check).
+template <class R>
+__device__ __forceinline__ uint32_t chain(typename R::Scalars& sc, uint32_t& sqv, uint32_t myc, uint32_t k,
+                                          const typename R::Win& win, uint32_t (*SNAP)[16], int lane, uint32_t& mvw,
+                                          uint32_t (&scw)[R::kVary]) {
+  using Sc = typename R::Scalars;
+  constexpr int kScw = sizeof(Sc) / 4;
+  reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
+  // the codes are in registers before the chain starts, so the loop head
+  // waits for nothing (its only LDS access is the snapshot byte store)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(myc) : "memory");
+  mvw = 0;
+#pragma unroll
+  for (int w = 0; w < R::kVary; ++w) scw[w] = 0;
+  uint32_t kplay = k;
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint32_t code = lane_value(myc, (int)j);
+    uint32_t mv;
+    if ((code & kTokBad) || !R::step(sc, win, j, code, sqv, lane, mv)) {
+      kplay = j;
+      break;
+    }
+    reinterpret_cast<uint8_t*>(SNAP[j + 1])[lane] = (uint8_t)sqv;
+    const bool mine = (uint32_t)lane == j;
+    mvw = mine ? mv : mvw;
+    uint32_t cur[kScw];
+    __builtin_memcpy(cur, &sc, sizeof(Sc));
+#pragma unroll
+    for (int w = 0; w < R::kVary; ++w) scw[w] = mine ? cur[w] : scw[w];
+  }
+  lds_fence();
+  return kplay;
+}
+
+// Lane j checks move j of a chained window against the board before it and
+// packs the board after it (records o1 + j).  Returns the first failing move
+// (>= k: none).
+template <class R>
+__device__ __forceinline__ uint32_t check(const typename R::Scalars& sc0, const typename R::Win& win,
+                                          const uint32_t (*SNAP)[16], uint32_t kplay, uint32_t k, uint32_t mvw,
+                                          const uint32_t (&scw)[R::kVary], int lane, typename R::Pos* __restrict__ out,
+                                          typename R::Board* __restrict__ states, uint32_t o1) {
+  using Sc = typename R::Scalars;
+  constexpr int kScw = sizeof(Sc) / 4;
+  bool fail = false;
+  // scalars before move j: after move j - 1, or the window's own; the words
+  // the chain does not collect follow from the window's first
+  uint32_t sb[kScw], sa[kScw];
+  __builtin_memcpy(sb, &sc0, sizeof(Sc));
+  __builtin_memcpy(sa, &sc0, sizeof(Sc));
+#pragma unroll
+  for (int w = 0; w < R::kVary; ++w) {
+    const uint32_t up = (uint32_t)__shfl_up((int)scw[w], 1, 64);
+    sb[w] = lane == 0 ? sb[w] : up;
+    sa[w] = scw[w];
+  }
+  if ((uint32_t)lane < kplay) {
+    Sc before_sc, after_sc;
+    __builtin_memcpy(&before_sc, sb, sizeof(Sc));
+    __builtin_memcpy(&after_sc, sa, sizeof(Sc));
+    R::fix(before_sc, sc0, win, (uint32_t)lane, false);
+    R::fix(after_sc, sc0, win, (uint32_t)lane, true);
+    uint32_t wb[16], wa[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      wb[i] = SNAP[lane][i];
+      wa[i] = SNAP[lane + 1][i];
+    }
+    fail = !R::verify(R::board_from(wb, before_sc), R::unpack_move(mvw));
+    if (!fail) {
+      const uint32_t o = o1 + lane;
+      if (out) out[o] = R::pack_from(wa, after_sc);
+      if (states) states[o] = R::board_from(wa, after_sc);
+    }
+  }
+  const uint64_t fails = __ballot(fail);
+  return fails ? (uint32_t)__builtin_ctzll(fails) : kplay;
+}
+
+// kFinal* of the last board (its bytes in B), its legal-move search split
+// over the lanes by from-square.
+template <class R>
+__device__ __forceinline__ uint8_t final_flags(const uint32_t* B, const typename R::Scalars& sc, int lane) {
+  uint32_t wl[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) wl[i] = B[i];
+  const typename R::Board last = in_vgprs(R::board_from(wl, sc));
+  const bool any = __ballot(R::any_legal_from(last, lane, lane == 0)) != 0;
+  return R::end_flags(last, any);
+}
+
+// ---- one wave per game ----
 template <class R>
 __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char* __restrict__ text,
                                                          const uint32_t* __restrict__ fen_off,
@@ -170,7 +372,6 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
                                                          uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
   using Board = typename R::Board;
   using Sc = typename R::Scalars;
-  constexpr int kScw = sizeof(Sc) / 4;
   static_assert(sizeof(Sc) % 4 == 0, "scalars as dwords");
   __shared__ uint32_t SNAP[65][16];  // byte s of SNAP[j] = square s before the window's move j
   __shared__ uint32_t TK[kTokRing];  // pending token codes
@@ -185,30 +386,8 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     return;
   }
   const uint32_t nmoves = nply - 1;
-
-  // ---- root: FEN through LDS, parsed by every lane alike ----
   Board root;
-  bool ok;
-  {
-    // The FEN goes through the move-text buffer (free until tokenising
-    // starts); one longer than it (kTxt characters: a legal FEN has < 100)
-    // is rejected as unparsable.
-    const uint32_t flen = m0 - f0;
-    ok = flen <= (uint32_t)kTxt;
-    if (ok) {
-      for (uint32_t i = lane; i < flen; i += 64) TXT[i] = text[f0 + i];
-      lds_fence();
-      // Most games start from the variant's standard position: recognised
-      // by one lane-parallel compare, its board is a constant (the parser's
-      // own result, tests/test_gpu_builder.py); any other FEN is parsed.
-      const char* sf = R::start_fen(variant);
-      const uint32_t sl = R::start_fen_len(variant);
-      const bool same = flen == sl && __ballot((uint32_t)lane < sl && TXT[lane] != sf[lane]) == 0;
-      if (same) root = R::start_board(variant);
-      else ok = R::parse_fen(TXT, 0, flen, variant, root);
-    }
-  }
-  if (!ok) {
+  if (!root_board<R>(variant, text, f0, m0, TXT, lane, root)) {
     if (lane == 0) latch(err, kBuildErrFen, g, 0);
     return;
   }
@@ -216,133 +395,25 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     if (out) out[o0] = R::pack(root);
     if (states) states[o0] = root;
   }
-  // The chain keeps the board as lane bytes — lane l holds square l's piece
-  // (sqv), so a move is a handful of lane-parallel selects — plus the
-  // wave-uniform scalars (side to move, castling rooks, en passant, pockets).
-  // Each ply's board is one byte per lane into SNAP; the checking lanes turn
-  // snapshots back into bitboards.
   Sc sc = first_lane(R::scalars(root));
   uint32_t sqv = R::lane_square(root, lane);
-  reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
-
-  // ---- windows of up to 64 moves ----
-  uint32_t p = m0;   // next text character to tokenise
-  uint32_t tbase = 0;  // text offset of TXT[0]
-  bool staged = false;
-  char prev = ' ';   // the character before p
-  uint32_t ntok = 0; // pending codes in TK[0 .. ntok)
-  uint32_t done = 0; // moves played and checked
-  uint32_t bad = 0;  // kBuildErr* of this game
-  uint32_t bad_ply = 0;
+  // windows of up to 64 moves: tokenise, chain, check
+  Tok t{m0, 0u, 0u, false, ' '};
+  uint32_t done = 0, bad = 0, bad_ply = 0;
   while (done < nmoves) {
-    // (a) tokenise until a full window is pending or the text ends; the
-    // characters come from an LDS copy of the move text (kTxt at a time,
-    // loaded with independent loads), so a token's tail is an LDS read
-    while (ntok < 64 && p < e) {
-      if (!staged || p + 64 + 6 > tbase + (uint32_t)kTxt) {
-        tbase = p;
-        staged = true;
-        const uint32_t lim = min((uint32_t)kTxt, e - tbase + 72);  // the text, then spaces for any token tail
-        for (uint32_t q = lane; q < lim; q += 64) TXT[q] = tbase + q < e ? text[tbase + q] : ' ';
-        lds_fence();
-      }
-      const uint32_t i = p - tbase + lane;
-      const char c = TXT[i];
-      const char cprev = (char)__shfl_up((int)c, 1, 64);
-      const bool start = !space(c) && space(lane == 0 ? prev : cprev);
-      const uint64_t starts = __ballot(start);
-      if (start) {
-        char t[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) t[q] = TXT[i + q];
-        int len = 1;
-        bool more = true;
-#pragma unroll
-        for (int q = 1; q < 6; ++q) {
-          more = more && !space(t[q]);
-          len += more ? 1 : 0;
-        }
-        const uint32_t code = (len == 4 || len == 5) ? R::encode(t, len) : kTokBad;
-        const uint32_t idx = ntok + (uint32_t)__popcll(starts & ((1ull << lane) - 1));
-        if (idx < (uint32_t)kTokRing) TK[idx] = code;
-      }
-      ntok += (uint32_t)__popcll(starts);
-      prev = (char)__shfl((int)c, 63, 64);
-      p += 64;
-    }
-    lds_fence();
-    if (ntok == 0 || ntok > (uint32_t)kTokRing) {  // fewer tokens than the host counted (or a ring overrun)
+    tokenise<R>(t, text, e, TXT, TK, 64, lane);
+    if (t.ntok == 0 || t.ntok > (uint32_t)kTokRing) {  // fewer tokens than the host counted (or a ring overrun)
       bad = kBuildErrCount;
       bad_ply = done + 1;
       break;
     }
-    const uint32_t k = min(min(ntok, 64u), nmoves - done);
-    // (b) the chain, wave-uniform: interpret and play each move.  Lane j
-    // collects move j's code, the move and the scalars after it,
-    // SNAP[j + 1] the board after it.
+    const uint32_t k = min(min(t.ntok, 64u), nmoves - done);
     const uint32_t myc = TK[lane];
-    // the codes are in registers before the chain starts, so the loop head
-    // waits for nothing (its only LDS access is the snapshot byte store)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(myc) : "memory");
     const Sc sc0 = sc;
     const typename R::Win win = R::window(sc, myc, k, lane);
-    uint32_t mvw = 0;
-    uint32_t scw[R::kVary];
-#pragma unroll
-    for (int w = 0; w < R::kVary; ++w) scw[w] = 0;
-    uint32_t kplay = k;
-    for (uint32_t j = 0; j < k; ++j) {
-      const uint32_t code = lane_value(myc, (int)j);
-      uint32_t mv;
-      if ((code & kTokBad) || !R::step(sc, win, j, code, sqv, lane, mv)) {
-        kplay = j;
-        break;
-      }
-      reinterpret_cast<uint8_t*>(SNAP[j + 1])[lane] = (uint8_t)sqv;
-      const bool mine = (uint32_t)lane == j;
-      mvw = mine ? mv : mvw;
-      uint32_t cur[kScw];
-      __builtin_memcpy(cur, &sc, sizeof(Sc));
-#pragma unroll
-      for (int w = 0; w < R::kVary; ++w) scw[w] = mine ? cur[w] : scw[w];
-    }
-    lds_fence();
-    // (c) lane j checks move j against the board before it and packs the board after it
-    bool fail = false;
-    {
-      // scalars before move j: after move j - 1, or the window's own; the
-      // words the chain does not collect follow from the window's first
-      uint32_t sb[kScw], sa[kScw];
-      __builtin_memcpy(sb, &sc0, sizeof(Sc));
-      __builtin_memcpy(sa, &sc0, sizeof(Sc));
-#pragma unroll
-      for (int w = 0; w < R::kVary; ++w) {
-        const uint32_t up = (uint32_t)__shfl_up((int)scw[w], 1, 64);
-        sb[w] = lane == 0 ? sb[w] : up;
-        sa[w] = scw[w];
-      }
-      if ((uint32_t)lane < kplay) {
-        Sc before_sc, after_sc;
-        __builtin_memcpy(&before_sc, sb, sizeof(Sc));
-        __builtin_memcpy(&after_sc, sa, sizeof(Sc));
-        R::fix(before_sc, sc0, win, (uint32_t)lane, false);
-        R::fix(after_sc, sc0, win, (uint32_t)lane, true);
-        uint32_t wb[16], wa[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          wb[i] = SNAP[lane][i];
-          wa[i] = SNAP[lane + 1][i];
-        }
-        fail = !R::verify(R::board_from(wb, before_sc), R::unpack_move(mvw));
-        if (!fail) {
-          const uint32_t o = o0 + done + lane + 1;
-          if (out) out[o] = R::pack_from(wa, after_sc);
-          if (states) states[o] = R::board_from(wa, after_sc);
-        }
-      }
-    }
-    const uint64_t fails = __ballot(fail);
-    const uint32_t first = fails ? (uint32_t)__builtin_ctzll(fails) : kplay;
+    uint32_t mvw, scw[R::kVary];
+    const uint32_t kplay = chain<R>(sc, sqv, myc, k, win, SNAP, lane, mvw, scw);
+    const uint32_t first = check<R>(sc0, win, SNAP, kplay, k, mvw, scw, lane, out, states, o0 + done + 1);
     if (first < k) {
       bad = kBuildErrMove;
       bad_ply = done + first + 1;
@@ -350,50 +421,213 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     }
     R::advance(sc, win, k);
     done += k;
-    ntok -= k;
-    // drop the consumed codes; the next window starts from the board after
-    // this one's last move (the lanes' bytes)
-    uint32_t keep[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const uint32_t src = k + lane + 64 * r;
-      keep[r] = src < (uint32_t)kTokRing ? TK[src] : 0;
-    }
-    lds_fence();
-    reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-      if ((uint32_t)lane + 64 * r < ntok) TK[lane + 64 * r] = keep[r];
-    lds_fence();
+    tok_consume(t, TK, k, lane);
   }
-  if (!bad) {
-    // text left after the host's count: more tokens than plies
-    bool extra = ntok != 0;
-    for (uint32_t q = p; q < e && !extra; q += 64) {
-      const uint32_t i = q + lane;
-      const char c = i < e ? text[i] : ' ';
-      const char cprev = (char)__shfl_up((int)c, 1, 64);
-      extra = __ballot(!space(c) && space(lane == 0 ? prev : cprev)) != 0;
-      prev = (char)__shfl((int)c, 63, 64);
-    }
-    if (extra) {
-      bad = kBuildErrCount;
-      bad_ply = nmoves + 1;
-    }
+  if (!bad && tok_extra(t, text, e, lane)) {  // text left after the host's count: more tokens than plies
+    bad = kBuildErrCount;
+    bad_ply = nmoves + 1;
   }
   if (bad) {
     if (lane == 0) latch(err, bad, g, bad_ply);
     return;
   }
   if (final) {
+    reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
     lds_fence();
-    uint32_t wl[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) wl[i] = SNAP[0][i];
-    const Board last = in_vgprs(R::board_from(wl, sc));
-    const bool any = __ballot(R::any_legal_from(last, lane, lane == 0)) != 0;
-    if (lane == 0) final[g] = R::end_flags(last, any);
+    const uint8_t f = final_flags<R>(SNAP[0], sc, lane);
+    if (lane == 0) final[g] = f;
   }
+}
+
+// ---- two waves per game (latency: a few games per call) ----
+// Wave 0 runs the chain of window s while wave 1 checks window s - 1 and
+// tokenises window s + 1 (double-buffered snapshots, codes and chain
+// outputs in LDS, one workgroup barrier per window); the last window's check
+// runs beside the game-end flags.  Same records, errors and flags as the
+// one-wave kernel, in about 0.7 of its time for one game (the chain alone is
+// the critical path), but twice its waves: for calls of up to a round of the
+// device's wave slots.
+template <class R>
+struct PairLds {
+  using Sc = typename R::Scalars;
+  static constexpr int kScw = sizeof(Sc) / 4;
+  static constexpr int kWinW = sizeof(typename R::Win) / 4 > 0 ? sizeof(typename R::Win) / 4 : 1;
+  uint32_t SNAP[2][65][16];
+  uint32_t TKW[2][64];          // the window's codes
+  uint32_t MV[2][64];           // chain outputs per lane: move, scalars, Win
+  uint32_t SCW[2][R::kVary][64];
+  uint32_t WIN[2][kWinW][64];
+  uint32_t SC0[2][kScw];        // the window's first scalars
+  uint32_t KW[2], KP[2];        // codes, moves played
+  uint32_t TK[kTokRing];        // the tokeniser's ring
+  uint32_t FIN[16];             // the last board's bytes
+  uint32_t nw, cnt_ply, bad, bad_ply;
+  char TXT[kTxt];
+};
+
+template <class R>
+__global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const char* __restrict__ text,
+                                                          const uint32_t* __restrict__ fen_off,
+                                                          const uint32_t* __restrict__ mv_off, uint32_t ngames,
+                                                          const uint32_t* __restrict__ ply_off,
+                                                          typename R::Pos* __restrict__ out,
+                                                          typename R::Board* __restrict__ states,
+                                                          uint32_t* __restrict__ err, uint8_t* __restrict__ final) {
+  using Board = typename R::Board;
+  using Sc = typename R::Scalars;
+  using Win = typename R::Win;
+  using L_t = PairLds<R>;
+  constexpr int kScw = L_t::kScw, kWinW = L_t::kWinW;
+  __shared__ L_t L;
+  const uint32_t g = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (g >= ngames) return;
+  const uint32_t f0 = fen_off[g], m0 = mv_off[g], e = fen_off[g + 1];
+  const uint32_t o0 = ply_off[g], nply = ply_off[g + 1] - o0;
+  if (nply == 0) {
+    if (threadIdx.x == 0) latch(err, kBuildErrCount, g, 0);
+    return;
+  }
+  const uint32_t nmoves = nply - 1;
+  const uint32_t nw0 = (nmoves + 63) / 64;
+  // wave 0: the root; wave 1 waits (the FEN goes through TXT, which wave 1
+  // then uses for the move text)
+  Sc sc;
+  uint32_t sqv = 0;
+  if (wv == 0) {
+    Board root;
+    const bool ok = root_board<R>(variant, text, f0, m0, L.TXT, lane, root);
+    if (lane == 0) {
+      L.bad = ok ? 0u : kBuildErrFen;
+      L.bad_ply = 0;
+      L.cnt_ply = 0;
+      L.nw = nw0;
+      if (ok && out) out[o0] = R::pack(root);
+      if (ok && states) states[o0] = root;
+    }
+    if (ok) {
+      sc = first_lane(R::scalars(root));
+      sqv = R::lane_square(root, lane);
+    }
+  }
+  __syncthreads();
+  if (L.bad) {
+    if (threadIdx.x == 0) latch(err, L.bad, g, 0);
+    return;
+  }
+  // wave 1: the codes of window w (k = its moves, fewer when the text ends:
+  // a count error, reported after the earlier windows' checks)
+  Tok t{m0, 0u, 0u, false, ' '};
+  auto produce = [&](uint32_t w) {
+    const uint32_t need = min(64u, nmoves - 64 * w);
+    tokenise<R>(t, text, e, L.TXT, L.TK, need, lane);
+    const uint32_t got = t.ntok > (uint32_t)kTokRing ? 0u : min(t.ntok, need);  // (0: a ring overrun)
+    L.TKW[w & 1][lane] = (uint32_t)lane < got ? L.TK[lane] : 0u;
+    lds_fence();
+    if (lane == 0) L.KW[w & 1] = got;
+    if (got < need) {  // the text ended: this window is the game's last
+      if (lane == 0) {
+        L.cnt_ply = 64 * w + got + 1;
+        L.nw = w + 1;
+      }
+    } else {
+      tok_consume(t, L.TK, got, lane);
+      if (w + 1 == nw0 && tok_extra(t, text, e, lane) && lane == 0) L.cnt_ply = nmoves + 1;
+    }
+  };
+  if (wv == 1 && nw0 > 0) produce(0);
+  __syncthreads();
+  uint8_t fl = 0;
+  for (uint32_t s = 0;; ++s) {
+    const uint32_t nw = L.nw;
+    if (wv == 0) {
+      if (s < nw) {
+        const uint32_t b = s & 1, k = L.KW[b];
+        const uint32_t myc = L.TKW[b][lane];
+        const Win win = R::window(sc, myc, k, lane);
+        uint32_t sw[kScw];
+        __builtin_memcpy(sw, &sc, sizeof(Sc));
+        uint32_t mvw, scw[R::kVary];
+        const uint32_t kplay = chain<R>(sc, sqv, myc, k, win, L.SNAP[b], lane, mvw, scw);
+        L.MV[b][lane] = mvw;
+#pragma unroll
+        for (int w = 0; w < R::kVary; ++w) L.SCW[b][w][lane] = scw[w];
+        uint32_t ww[kWinW] = {};
+        if constexpr (sizeof(Win) >= 4) __builtin_memcpy(ww, &win, sizeof(Win));
+#pragma unroll
+        for (int w = 0; w < kWinW; ++w) L.WIN[b][w][lane] = ww[w];
+        if (lane < kScw) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int w = 0; w < kScw; ++w) v = lane == w ? sw[w] : v;
+          L.SC0[b][lane] = v;
+        }
+        if (lane == 0) L.KP[b] = kplay;
+        R::advance(sc, win, k);
+      } else if (s == nw && final) {
+        reinterpret_cast<uint8_t*>(L.FIN)[lane] = (uint8_t)sqv;
+        lds_fence();
+        fl = final_flags<R>(L.FIN, sc, lane);
+      }
+    } else {
+      if (s >= 1 && s - 1 < nw) {
+        const uint32_t w0 = s - 1, b = w0 & 1, k = L.KW[b], kplay = L.KP[b];
+        Sc sc0;
+        uint32_t sw[kScw];
+#pragma unroll
+        for (int w = 0; w < kScw; ++w) sw[w] = L.SC0[b][w];
+        __builtin_memcpy(&sc0, sw, sizeof(Sc));
+        Win win;
+        uint32_t ww[kWinW];
+#pragma unroll
+        for (int w = 0; w < kWinW; ++w) ww[w] = L.WIN[b][w][lane];
+        if constexpr (sizeof(Win) >= 4) __builtin_memcpy(&win, ww, sizeof(Win));
+        uint32_t scw[R::kVary];
+#pragma unroll
+        for (int w = 0; w < R::kVary; ++w) scw[w] = L.SCW[b][w][lane];
+        const uint32_t first = check<R>(sc0, win, L.SNAP[b], kplay, k, L.MV[b][lane], scw, lane, out, states,
+                                        o0 + 64 * w0 + 1);
+        if (first < k && lane == 0) {
+          L.bad = kBuildErrMove;
+          L.bad_ply = 64 * w0 + first + 1;
+        }
+      }
+      if (s + 1 < nw) produce(s + 1);
+    }
+    __syncthreads();
+    if (L.bad || s >= L.nw) break;
+  }
+  if (threadIdx.x == 0) {
+    if (L.bad) latch(err, L.bad, g, L.bad_ply);
+    else if (L.cnt_ply) latch(err, kBuildErrCount, g, L.cnt_ply);
+    else if (final) final[g] = fl;
+  }
+}
+
+// Two waves per game up to kPairGames games (a call that fits one round of
+// wave slots: latency), one wave per game above (throughput).
+// FNNUE_REPLAY_PAIR_MAX overrides the bound (A/B only).
+constexpr uint32_t kPairGames = 1024;
+inline uint32_t pair_games_max() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("FNNUE_REPLAY_PAIR_MAX");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : kPairGames;
+  }();
+  return v;
+}
+template <class R>
+hipError_t launch_replay(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
+                         uint32_t ngames, const uint32_t* d_ply_off, typename R::Pos* d_out,
+                         typename R::Board* d_states, uint32_t* d_err, uint8_t* d_final, hipStream_t s) {
+  if (!ngames) return hipSuccess;
+  if (ngames <= pair_games_max())
+    hipLaunchKernelGGL(replay_pair_kernel<R>, dim3(ngames), dim3(128), 0, s, variant, d_text, d_fen_off, d_mv_off,
+                       ngames, d_ply_off, d_out, d_states, d_err, d_final);
+  else
+    hipLaunchKernelGGL(replay_wave_kernel<R>, dim3(ngames), dim3(64), 0, s, variant, d_text, d_fen_off, d_mv_off,
+                       ngames, d_ply_off, d_out, d_states, d_err, d_final);
+  return hipGetLastError();
 }
 
 }  // namespace replay

@@ -346,11 +346,8 @@ __global__ void vwrite_children_kernel(const vb::VBoard* __restrict__ states, ui
 hipError_t replay_vgames_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,
                                 const uint32_t* d_ply_off, uint32_t ngames, fnnue_vpos* d_out, void* d_states,
                                 uint8_t* d_final, uint32_t* d_err, hipStream_t s) {
-  if (!ngames) return hipSuccess;
-  hipLaunchKernelGGL(replay::replay_wave_kernel<VariantRules>, dim3(ngames), dim3(64), 0, s, variant, d_text,
-                     d_fen_off, d_mv_off, ngames, d_ply_off, d_out, static_cast<vb::VBoard*>(d_states), d_err,
-                     d_final);
-  return hipGetLastError();
+  return replay::launch_replay<VariantRules>(variant, d_text, d_fen_off, d_mv_off, ngames, d_ply_off, d_out,
+                                             static_cast<vb::VBoard*>(d_states), d_err, d_final, s);
 }
 
 BuildResult build_vbatch_device(int variant, const char* d_text, const uint32_t* d_fen_off, const uint32_t* d_mv_off,

@@ -1,7 +1,9 @@
 """Writes tools/exp/diag_replay_stamps.patch against the working tree: s_memtime
-stamps of game 0's replay phases (FEN, tokenising, board chain, check + pack,
-tail, game-end flags) into a device array read by fnnue_diag_replay_stamps
-(tools/diag/replay_stamps.py).  Diagnostic builds only (tools/exp_build.sh)."""
+stamps of game 0's replay phases in the one-wave kernel (FEN, tokenising, board
+chain, check + pack, tail, game-end flags) into a device array read by
+fnnue_diag_replay_stamps (tools/diag/replay_stamps.py; run it with
+FNNUE_REPLAY_PAIR_MAX=0 so that every call takes the one-wave kernel).
+Diagnostic builds only (tools/exp_build.sh)."""
 import difflib
 import os
 
@@ -24,22 +26,17 @@ s = sub(s, "  const uint32_t nmoves = nply - 1;\n",
         "  unsigned long long T0 = __builtin_amdgcn_s_memtime(), Tk = T0, acc[6] = {0, 0, 0, 0, 0, 0};\n"
         "#define STAMP(i) do { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); acc[i] += n_ - Tk; "
         "Tk = n_; } while (0)\n")
-s = sub(s, "  // ---- windows of up to 64 moves ----", "  STAMP(0);\n  // ---- windows of up to 64 moves ----")
-s = sub(s, "    lds_fence();\n    if (ntok == 0 || ntok > (uint32_t)kTokRing) {",
-        "    lds_fence();\n    STAMP(1);\n    if (ntok == 0 || ntok > (uint32_t)kTokRing) {")
-s = sub(s, "    lds_fence();\n    // (c) lane j checks move j", "    lds_fence();\n    STAMP(2);\n    // (c) lane j checks move j")
-s = sub(s, "    const uint64_t fails = __ballot(fail);", "    const uint64_t fails = __ballot(fail);\n    STAMP(3);")
-s = sub(s, "  if (final) {\n", "  STAMP(4);\n  if (final) {\n")
-if os.environ.get("CHAIN_SPLIT"):
-    # inside the chain: interpret | play | store (acc[2] = the rest of (b))
-    s = sub(s, "      R::play(b, m, sqv, lane);\n", "      STAMP(2);\n      R::play(b, m, sqv, lane);\n      STAMP(6);\n")
-    s = sub(s, "        MV[j] = m;\n      }\n", "        MV[j] = m;\n      }\n      STAMP(7);\n")
-    s = s.replace("acc[6] = {0, 0, 0, 0, 0, 0}", "acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}")
-i = s.rindex("}\n\n}  // namespace replay")
-s = s[:i] + ("  STAMP(5);\n  if (diag) {\n    for (int i = 0; i < 6; ++i) g_stamp[i] = acc[i];\n"
-             "    g_stamp[6] = __builtin_amdgcn_s_memtime() - T0;\n    g_stamp[7] = nmoves;\n"
-             + ("    g_stamp[6] = acc[6]; g_stamp[7] = acc[7];\n" if os.environ.get("CHAIN_SPLIT") else "")
-             + "  }\n") + s[i:]
+# (the one-wave kernel, the file's first; FNNUE_REPLAY_PAIR_MAX=0 runs it for every call)
+s = sub(s, "  // windows of up to 64 moves: tokenise, chain, check", "  STAMP(0);\n  // windows of up to 64 moves: tokenise, chain, check")
+s = sub(s, "    tokenise<R>(t, text, e, TXT, TK, 64, lane);\n", "    tokenise<R>(t, text, e, TXT, TK, 64, lane);\n    STAMP(1);\n")
+s = sub(s, "    const uint32_t kplay = chain<R>(sc, sqv, myc, k, win, SNAP, lane, mvw, scw);\n",
+        "    const uint32_t kplay = chain<R>(sc, sqv, myc, k, win, SNAP, lane, mvw, scw);\n    STAMP(2);\n")
+s = sub(s, "o0 + done + 1);\n", "o0 + done + 1);\n    STAMP(3);\n")
+s = sub(s, "  if (final) {\n    reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;",
+        "  STAMP(4);\n  if (final) {\n    reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;")
+s = sub(s, "    if (lane == 0) final[g] = f;\n  }\n}\n",
+        "    if (lane == 0) final[g] = f;\n  }\n  STAMP(5);\n  if (diag) {\n    for (int i = 0; i < 6; ++i) g_stamp[i] = acc[i];\n"
+        "    g_stamp[6] = __builtin_amdgcn_s_memtime() - T0;\n    g_stamp[7] = nmoves;\n  }\n}\n")
 b = sub(orig_bh, "hipError_t perft_device(",
         'extern "C" int fnnue_diag_replay_stamps(unsigned long long* out) {\n'
         "  return hipMemcpyFromSymbol(out, HIP_SYMBOL(replay::g_stamp), 64) == hipSuccess ? 0 : -1;\n}\n\n"
