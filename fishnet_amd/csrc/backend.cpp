@@ -402,6 +402,7 @@ struct fnnue_backend {
   int device = 0;
   int32_t norm = kNormalizeToPawnSf151;
   size_t piece_plies = 524288;  // FNNUE_BACKEND_PIECE_PLIES
+  bool any_order = true;         // FNNUE_BACKEND_ANY_ORDER=0: wait for the nets' pieces in net order
   // The capacity-1 channel: a go() runs on its caller's thread holding run_mu,
   // so a second caller waits until the first call is answered
   // (mpsc::channel(1) with one message in flight, without a thread hand-off
@@ -946,10 +947,34 @@ void fnnue_backend::run(Job& j) {
       if (r >= 1 && r - 1 < net[k].pieces.size()) rc = stage_eval(k, r - 1);
     if (rc == FNNUE_OK && r >= 1 && r < rounds) rc = poll(false);
   }
-  for (bool left = true; rc == FNNUE_OK && left;) {
-    rc = poll(true);
-    left = false;
-    for (const NetWork& W : net) left = left || W.next < W.pieces.size();
+  // The rest, in the order the results come back: a net's pieces that are
+  // back are written while another net's are still on the device (the small
+  // variant nets' usually are back first); the host blocks only when a
+  // single net is left.
+  while (rc == FNNUE_OK) {
+    bool progress = false;
+    int first = -1, left = 0;
+    for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k) {
+      NetWork& W = net[k];
+      while (rc == FNNUE_OK && W.next < W.pieces.size()) {
+        bool ready = false;
+        rc = finish(j, k, false, &ready);
+        if (!ready) break;
+        progress = true;
+      }
+      if (W.next < W.pieces.size()) {
+        ++left;
+        if (first < 0) first = k;
+      }
+    }
+    if (rc || !left) break;
+    if (progress) continue;
+    if (left == 1 || !any_order) {
+      bool ready = false;
+      rc = finish(j, first, true, &ready);
+    } else {
+      for (int i = 0; i < 64; ++i) _mm_pause();
+    }
   }
   if (rc) {
     for (int k = 0; k < kKinds; ++k) {  // the pinned images stay in use until the copies are done
@@ -1044,6 +1069,7 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
     b->pool_threads = nt;
     b->trace = std::getenv("FNNUE_BACKEND_TRACE") != nullptr;
     if (const char* e = std::getenv("FNNUE_BACKEND_PIECE_PLIES")) b->piece_plies = (size_t)std::max(1024L, std::atol(e));
+    if (const char* e = std::getenv("FNNUE_BACKEND_ANY_ORDER")) b->any_order = std::atoi(e) != 0;
   }
   for (int k = 0; k < kKinds; ++k) {
     if (!slot[k]) continue;

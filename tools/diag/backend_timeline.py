@@ -29,11 +29,16 @@ ker = rows("*kernel_trace.csv")
 cpy = rows("*memory_copy_trace.csv")
 waits = ("hipStreamSynchronize", "hipEventSynchronize")
 actor = collections.Counter(r["Thread_Id"] for r in api if r["Function"] in waits).most_common(1)[0][0]
+# device guards / launch bookkeeping between a call's last wait and the next call's first copy
+quiet = ("__hipPushCallConfiguration", "__hipPopCallConfiguration", "hipGetLastError", "hipSetDevice",
+         "hipGetDevice", "hipEventQuery")
 calls, cur, in_wait = [], [], False
 for r in api:
     if r["Thread_Id"] != actor:
         continue
     f = r["Function"]
+    if f in quiet:
+        continue
     # a call ends with its last wait; the next non-wait API call starts the next one
     if f not in waits and in_wait and f in ("hipMemcpyAsync", "hipLaunchKernel") and cur and \
             cur[-1]["Function"] in waits:
