@@ -972,8 +972,10 @@ void fnnue_backend::run(Job& j) {
     if (left == 1 || !any_order) {
       bool ready = false;
       rc = finish(j, first, true, &ready);
-    } else {
+    } else {  // polling counts as waiting for the device
+      const auto tw = Clock::now();
       for (int i = 0; i < 64; ++i) _mm_pause();
+      wait_ms += ms_since(tw);
     }
   }
   if (rc) {

@@ -143,14 +143,16 @@ int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nba
  * host-to-device copy, the replay, the evaluation kernels and one device-to-
  * host copy of its results (plus the evaluator's error word), in order on the
  * net's stream; the host stages the next pieces and writes a piece's
- * responses while the device works on the later ones. */
+ * responses while the device works on the later ones, in the order the
+ * pieces come back (another net's may be written first), blocking only when
+ * a single net is left. */
 typedef struct {
   double prep_ms;         /* host: sizes, move-work roots, text staging, copies and kernels enqueued */
-  double device_ms;       /* host blocked waiting for the device */
+  double device_ms;       /* host waiting for the device (blocked, or polling the nets' pieces) */
   double fill_ms;         /* responses written (overlaps the device's later pieces) */
   double total_ms;
   uint64_t positions;     /* positions evaluated (analysis plies + move-work children) */
-  uint32_t stream_syncs;  /* host waits on an event, a stream or a blocking copy */
+  uint32_t stream_syncs;  /* host blocking waits on an event, a stream or a copy */
   uint32_t rebuilds;      /* extra passes after a batch failed (per failed batch, its piece only) */
   uint32_t host_threads;  /* threads for the staging / fill loops (FNNUE_BACKEND_THREADS, default <= 8) */
   uint32_t pieces;        /* pieces over all nets */

@@ -31,7 +31,7 @@ waits = ("hipStreamSynchronize", "hipEventSynchronize")
 actor = collections.Counter(r["Thread_Id"] for r in api if r["Function"] in waits).most_common(1)[0][0]
 # device guards / launch bookkeeping between a call's last wait and the next call's first copy
 quiet = ("__hipPushCallConfiguration", "__hipPopCallConfiguration", "hipGetLastError", "hipSetDevice",
-         "hipGetDevice", "hipEventQuery")
+         "hipGetDevice")
 calls, cur, in_wait = [], [], False
 for r in api:
     if r["Thread_Id"] != actor:
@@ -39,15 +39,15 @@ for r in api:
     f = r["Function"]
     if f in quiet:
         continue
-    # a call ends with its last wait; the next non-wait API call starts the next one
+    # a call ends with its last wait or event poll; the next copy or launch starts the next one
     if f not in waits and in_wait and f in ("hipMemcpyAsync", "hipLaunchKernel") and cur and \
-            cur[-1]["Function"] in waits:
+            cur[-1]["Function"] in waits + ("hipEventQuery",):
         calls.append(cur)
         cur = []
-    in_wait = f in waits
+    in_wait = f in waits or f == "hipEventQuery"
     cur.append(r)
 calls.append(cur)
-calls = [c for c in calls if any(r["Function"] in waits for r in c)]
+calls = [c for c in calls if any(r["Function"] in waits + ("hipEventQuery",) for r in c)]
 per = len(calls) // nph
 c = calls[(phase + 1) * per - 2]
 t0 = int(c[0]["Start_Timestamp"])

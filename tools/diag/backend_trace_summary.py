@@ -17,6 +17,8 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 waits = ("hipStreamSynchronize", "hipEventSynchronize")
 syncs = collections.Counter(r["Thread_Id"] for r in rows if r["Function"] in waits)
 actor = syncs.most_common(1)[0][0]
+quiet = ("__hipPushCallConfiguration", "__hipPopCallConfiguration", "hipGetLastError", "hipSetDevice",
+         "hipGetDevice")
 calls, cur, in_sync = [], [], False
 for r in rows:
     if r["Thread_Id"] != actor:
@@ -25,10 +27,12 @@ for r in rows:
     if f not in waits and in_sync and f in ("hipMemcpyAsync", "hipLaunchKernel"):
         calls.append(cur)
         cur = []
-    in_sync = f in waits if f not in ("hipEventQuery",) else in_sync
+    # device guards, launch bookkeeping and event polls leave the state as it is
+    if f not in quiet:  # a call ends with its last wait or event poll
+        in_sync = f in waits or f == "hipEventQuery"
     cur.append(r)
 calls.append(cur)
-calls = [c for c in calls if any(r["Function"] in waits for r in c)]
+calls = [c for c in calls if any(r["Function"] in waits + ("hipEventQuery",) for r in c)]
 # each phase = warm-up calls + 1 probe + `per` timed calls; the timed ones are the last `per`
 n_phase = len(calls) // len(phases)
 alloc = ("hipMalloc", "hipFree", "hipHostMalloc", "hipHostFree", "hipMallocAsync", "hipFreeAsync")
