@@ -577,7 +577,12 @@ __global__ __launch_bounds__(1024) void seg_scatter_kernel(const typename Fs::Po
 // of those eight launches is mostly its launch-to-launch gap: ~45 µs in all,
 // profiles/r05/backend/timeline_1batch.txt).  Global memory written by one
 // phase is read by the next from the same CU, ordered by the barrier.
-constexpr uint32_t kSegSmallPlan = 8192;
+// Its one workgroup walks the positions in rounds of 1024, so past ~2k
+// positions the eight-kernel chain is faster: engine-actor calls of 24 / 32 /
+// 48 / 64 batches (2.4k-6.3k plies) took 0.192 / 0.203 / 0.238 / 0.267 ms with
+// a limit of 8192 and 0.185 / 0.192 / 0.208 / 0.221 ms with 2048, calls of
+// 1-16 batches the same (profiles/r05/small_plan/).
+constexpr uint32_t kSegSmallPlan = 2048;
 template <class Fs>
 constexpr int seg_small_lds_words() {
   constexpr int kIB = SegCtr<Fs>::kIB;

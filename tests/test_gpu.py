@@ -351,13 +351,14 @@ def test_groups_of_unrelated_positions(ev_cache):
         assert np.array_equal(ps, ops) and np.array_equal(po, opo)
 
 
-@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 511, 513, 1025, 4097])
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 511, 513, 1025, 2047, 2048, 2049, 4097, 8193])
 def test_groups_ragged_sizes(ev_cache, n):
     """Batch sizes around the segment plan's 256-position scan blocks (refresh
-    counts per block, block scan, local scans): CHAIN plies and STAR children,
-    the last group cut short."""
+    counts per block, block scan, local scans) and either side of the
+    one-workgroup plan's limit (2048 positions): CHAIN plies and STAR
+    children, the last group cut short."""
     ev, on = ev_cache()
-    for mode, pm, count in ((N.GROUP_CHAIN, N.PLAYOUT_PLIES, 80), (N.GROUP_STAR, N.PLAYOUT_CHILDREN, 4)):
+    for mode, pm, count in ((N.GROUP_CHAIN, N.PLAYOUT_PLIES, 130), (N.GROUP_STAR, N.PLAYOUT_CHILDREN, 4)):
         pos, off = F.random_playouts(31, count, mode=pm, threads=8)
         assert len(pos) >= n
         pos = pos[:n]

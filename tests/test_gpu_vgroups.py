@@ -117,6 +117,25 @@ def test_vgroups_random_walks_incremental_equals_refresh(vc, variant):
     assert np.array_equal(ss[idx], ops) and np.array_equal(so[idx], opo)
 
 
+@pytest.mark.parametrize("variant", [ZH, AT])
+@pytest.mark.parametrize("n", [97, 2048, 2049])
+def test_vgroups_either_side_of_the_one_workgroup_plan(vc, variant, n):
+    """Calls of at most 2048 positions take the one-workgroup segment plan,
+    larger ones the kernel chain: both give the from-scratch results (CHAIN
+    and STAR over the same legal games, the last game cut short)."""
+    ev, on = vc(variant)
+    _, pos, off = legal_games(variant, 40, 900 + variant)
+    assert len(pos) >= n
+    pos = pos[:n]
+    off = np.concatenate([off[off < n], [n]]).astype(np.uint32)
+    ss, so = ev.eval_vpositions(pos)
+    for mode in (N.GROUP_CHAIN, N.GROUP_STAR):
+        gs, go = ev.eval_vgroups(pos, off, mode)
+        assert np.array_equal(gs, ss) and np.array_equal(go, so), mode
+    ops, opo, rc = on.eval_packed(pos, threads=8)
+    assert rc == 0 and np.array_equal(ss, ops) and np.array_equal(so, opo)
+
+
 def test_vgroups_device_end_to_end_from_the_device_builder(vc):
     """fnnue_build_vbatch_device -> fnnue_eval_vgroups_device: crazyhouse games
     never leave HBM as positions; every ply against the oracle."""
