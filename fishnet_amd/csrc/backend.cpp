@@ -39,12 +39,14 @@
 #include <string>
 #include <thread>
 #include <emmintrin.h>
+#include <sched.h>
 #include <vector>
 
 #include "board.h"
 #include "builder.h"
 #include "internal.h"
 #include "vboard.h"
+#include "workers.h"
 
 using namespace fnnue;
 using namespace fnnue::detail;
@@ -119,77 +121,6 @@ struct PinnedBuf {
     return reinterpret_cast<T*>(static_cast<char*>(p) + off);
   }
 };
-
-// A few host threads for the per-batch loops of large calls (the caller joins
-// in): chunks of [0, n) handed out by an atomic counter.
-class Workers {
- public:
-  void start(int n) {
-    for (int i = 1; i < n; ++i) th_.emplace_back([this] { loop(); });
-  }
-  void stop() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      quit_ = true;
-    }
-    cv_.notify_all();
-    for (std::thread& t : th_) t.join();
-    th_.clear();
-  }
-  // f(lo, hi) over [0, n) in chunks of `grain` items
-  void run(size_t n, size_t grain, const std::function<void(size_t, size_t)>& f) {
-    if (!n) return;
-    if (th_.empty() || n <= grain) {
-      f(0, n);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      task_ = &f;
-      total_ = n;
-      step_ = grain;
-      next_ = 0;
-      active_ = th_.size();
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_.wait(lk, [&] { return active_ == 0; });
-    task_ = nullptr;
-  }
-
- private:
-  void work() {
-    for (;;) {
-      const size_t lo = next_.fetch_add(step_);
-      if (lo >= total_) return;
-      (*task_)(lo, std::min(lo + step_, total_));
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    std::unique_lock<std::mutex> lk(mu_);
-    for (;;) {
-      cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
-      if (quit_) return;
-      seen = gen_;
-      lk.unlock();
-      work();
-      lk.lock();
-      if (--active_ == 0) done_.notify_all();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void(size_t, size_t)>* task_ = nullptr;
-  size_t total_ = 0, step_ = 1, active_ = 0;
-  std::atomic<size_t> next_{0};
-  uint64_t gen_ = 0;
-  bool quit_ = false;
-};
-
 
 // Whitespace-separated tokens of a NUL-terminated string — the builder's rule
 // (replay_wave.h: blanks are ' ', '\t', '\n', '\r'; a token starts at a
@@ -395,6 +326,22 @@ struct NetWork {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// CPUs this process may use: its affinity mask, capped by a cgroup v2 CPU
+// quota (a container's share of a large host)
+int usable_cpus() {
+  int n = (int)std::max(1u, std::thread::hardware_concurrency());
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long period = 0;
+    if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0)
+      n = std::max(1, std::min(n, (int)((std::atol(quota) + period - 1) / period)));
+    std::fclose(f);
+  }
+  return n;
+}
+
 }  // namespace
 
 struct fnnue_backend {
@@ -403,6 +350,8 @@ struct fnnue_backend {
   int32_t norm = kNormalizeToPawnSf151;
   size_t piece_plies = 524288;  // FNNUE_BACKEND_PIECE_PLIES
   bool any_order = true;         // FNNUE_BACKEND_ANY_ORDER=0: wait for the nets' pieces in net order
+  size_t tail_plies = 0;         // FNNUE_BACKEND_TAIL_PLIES: a net's last piece cut to about this many
+  size_t fill_grain = 64;        // FNNUE_BACKEND_FILL_GRAIN: games per fill task
   // The capacity-1 channel: a go() runs on its caller's thread holding run_mu,
   // so a second caller waits until the first call is answered
   // (mpsc::channel(1) with one message in flight, without a thread hand-off
@@ -528,6 +477,21 @@ int fnnue_backend::plan(Job& j, int k) {
     plies += j.off[i + 1] - j.off[i];
   }
   if (plies >= (1ull << 31)) return fail(FNNUE_E_ARG, "batch too large");
+  // A short last piece: its fill is the one the device cannot hide
+  if (tail_plies && W.pieces.size() > 1) {
+    Piece& L = W.pieces.back();
+    size_t t = 0, cut = L.games.size();
+    while (cut > 1 && t < tail_plies) {
+      --cut;
+      t += j.off[L.games[cut] + 1] - j.off[L.games[cut]];
+    }
+    if (cut > 1 && cut < L.games.size()) {
+      Piece T;
+      T.games.assign(L.games.begin() + (long)cut, L.games.end());
+      L.games.resize(cut);
+      W.pieces.push_back(std::move(T));
+    }
+  }
   if (W.nk) {
     if (W.pieces.empty()) W.pieces.emplace_back();
     W.pieces.back().kids = true;
@@ -750,7 +714,7 @@ void fnnue_backend::fill(Job& j, int k, const Piece& P) {
   const uint64_t ms = (uint64_t)el;
   const uint32_t nps = el > 0 ? (uint32_t)std::min(4.0e9, (double)filled / (el * 1e-3)) : 0;
   const int32_t nrm = norm;
-  pool.run(P.ng, 64, [&](size_t lo, size_t hi) {
+  pool.run(P.ng, fill_grain, [&](size_t lo, size_t hi) {
     for (size_t g = lo; g < hi; ++g) {
       const size_t i = P.games[g];
       const uint32_t b = j.off[i], len = j.off[i + 1] - b;
@@ -1064,14 +1028,18 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
   b->device = device;
   if (init && init->normalize_to_pawn > 0) b->norm = init->normalize_to_pawn;
   {
-    // host threads for the text staging and response fill of large calls
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    int nt = (int)std::min(8u, hw);
+    // host threads for the text staging and response fill of large calls: up
+    // to 8, at most the CPUs this process may run on (12 or 16: within the
+    // box-to-box noise at 16384 batches per call, slower at 1024,
+    // profiles/r05/backend_threads/)
+    int nt = std::min(8, usable_cpus());
     if (const char* e = std::getenv("FNNUE_BACKEND_THREADS")) nt = std::max(1, std::min(64, std::atoi(e)));
     b->pool_threads = nt;
     b->trace = std::getenv("FNNUE_BACKEND_TRACE") != nullptr;
     if (const char* e = std::getenv("FNNUE_BACKEND_PIECE_PLIES")) b->piece_plies = (size_t)std::max(1024L, std::atol(e));
     if (const char* e = std::getenv("FNNUE_BACKEND_ANY_ORDER")) b->any_order = std::atoi(e) != 0;
+    if (const char* e = std::getenv("FNNUE_BACKEND_TAIL_PLIES")) b->tail_plies = (size_t)std::max(0L, std::atol(e));
+    if (const char* e = std::getenv("FNNUE_BACKEND_FILL_GRAIN")) b->fill_grain = (size_t)std::max(1L, std::atol(e));
   }
   for (int k = 0; k < kKinds; ++k) {
     if (!slot[k]) continue;

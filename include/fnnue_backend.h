@@ -154,7 +154,7 @@ typedef struct {
   uint64_t positions;     /* positions evaluated (analysis plies + move-work children) */
   uint32_t stream_syncs;  /* host blocking waits on an event, a stream or a copy */
   uint32_t rebuilds;      /* extra passes after a batch failed (per failed batch, its piece only) */
-  uint32_t host_threads;  /* threads for the staging / fill loops (FNNUE_BACKEND_THREADS, default <= 8) */
+  uint32_t host_threads;  /* threads for the staging / fill loops (FNNUE_BACKEND_THREADS; default: the usable CPUs, at most 8) */
   uint32_t pieces;        /* pieces over all nets */
 } fnnue_backend_stats;
 
