@@ -14,7 +14,7 @@ for v in "$@"; do
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
-    n = r["Name"].split("(")[0].replace("void ", "").replace("fnnue::", "").replace("(anonymous namespace)::", "")
+    n = r["Name"].replace("(anonymous namespace)::", "").replace("void ", "").replace("fnnue::", "").split("(")[0]
     print(f"{sys.argv[2]:8s} {n[:70]:70s} {r['Calls']:>5} {float(r['AverageNs'])/1e3:8.2f} us")
 PY
 done
