@@ -721,7 +721,11 @@ void fnnue_backend::fill(Job& j, int k, const Piece& P) {
       const uint8_t matrix = j.batches[i].multipv > 0 ? 1 : 0;  // Work::matrix_wanted: multipv is Some
       const bool sk = bskip[i];
       for (uint32_t q = 0; q < len; ++q) {
-        fnnue_position_response r;
+        // written in place: a response built on the stack and copied out
+        // stalls each wide load of the copy on the narrow stores before it
+        // (store forwarding: 1.8x the fill's time on the build host's CPU;
+        // on the GPU box's EPYC within the noise, profiles/r05/backend_fill/)
+        fnnue_position_response& r = j.out[b + q];
         std::memset(&r, 0, sizeof(r));
         r.position_id = q;
         r.time_ms = ms;
@@ -730,17 +734,17 @@ void fnnue_backend::fill(Job& j, int k, const Piece& P) {
           r.skipped = 1;
         } else {
           const size_t x = ply[g] + q;
+          const int32_t a = ps[x], c = po[x];
           r.matrix = matrix;
-          r.psqt = ps[x];
-          r.positional = po[x];
+          r.psqt = a;
+          r.positional = c;
           r.score_kind = FNNUE_SCORE_CP;
-          r.score = to_cp(r.psqt, r.positional, nrm);
+          r.score = to_cp(a, c, nrm);
           r.nodes = 1;
           // The last ply is the only one that can have no legal move (nothing
           // can be played from it): mate 0 / cp 0 instead of an evaluation.
           if (q + 1 == len && (fin[g] & kFinalNoMoves)) terminal_response(r, fin[g]);
         }
-        j.out[b + q] = r;
       }
     }
   });
