@@ -352,6 +352,8 @@ struct fnnue_backend {
   bool any_order = true;         // FNNUE_BACKEND_ANY_ORDER=0: wait for the nets' pieces in net order
   size_t tail_plies = 0;         // FNNUE_BACKEND_TAIL_PLIES: a net's last piece cut to about this many
   size_t fill_grain = 64;        // FNNUE_BACKEND_FILL_GRAIN: games per fill task
+  size_t size_grain = 256;       // FNNUE_BACKEND_SIZE_GRAIN: batches per sizing task
+  size_t stage_grain = 512;      // FNNUE_BACKEND_STAGE_GRAIN: games per text-staging task
   // The capacity-1 channel: a go() runs on its caller's thread holding run_mu,
   // so a second caller waits until the first call is answered
   // (mpsc::channel(1) with one message in flight, without a thread hand-off
@@ -537,7 +539,7 @@ int fnnue_backend::stage_up(Job& j, int k, size_t pi) {
   }
   fo[P.ng] = text;
   po[P.ng] = acc;
-  pool.run(P.ng, 512, [&](size_t lo, size_t hi) {
+  pool.run(P.ng, stage_grain, [&](size_t lo, size_t hi) {
     for (size_t g = lo; g < hi; ++g) {
       const size_t i = P.games[g];
       const fnnue_acquired& a = j.batches[i];
@@ -818,7 +820,7 @@ void fnnue_backend::run(Job& j) {
   // memory, so the next batches' are prefetched
   kind.resize(nb);
   bskip.resize(nb);
-  pool.run(nb, 256, [&](size_t lo, size_t hi) {
+  pool.run(nb, size_grain, [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) {
       if (i + 8 < hi) {
         __builtin_prefetch(j.batches[i + 8].moves);
@@ -1044,6 +1046,8 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
     if (const char* e = std::getenv("FNNUE_BACKEND_ANY_ORDER")) b->any_order = std::atoi(e) != 0;
     if (const char* e = std::getenv("FNNUE_BACKEND_TAIL_PLIES")) b->tail_plies = (size_t)std::max(0L, std::atol(e));
     if (const char* e = std::getenv("FNNUE_BACKEND_FILL_GRAIN")) b->fill_grain = (size_t)std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("FNNUE_BACKEND_SIZE_GRAIN")) b->size_grain = (size_t)std::max(1L, std::atol(e));
+    if (const char* e = std::getenv("FNNUE_BACKEND_STAGE_GRAIN")) b->stage_grain = (size_t)std::max(1L, std::atol(e));
   }
   for (int k = 0; k < kKinds; ++k) {
     if (!slot[k]) continue;
