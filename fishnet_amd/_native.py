@@ -17,7 +17,7 @@ FNNUE_OK = 0
 ERRORS = {
     -1: "FNNUE_E_ARG", -2: "FNNUE_E_IO", -3: "FNNUE_E_FORMAT", -4: "FNNUE_E_ARCH",
     -5: "FNNUE_E_DEVICE", -6: "FNNUE_E_POSITION", -7: "FNNUE_E_OOM", -8: "FNNUE_E_MOVE",
-    -9: "FNNUE_E_FEN", -10: "FNNUE_E_CAPACITY",
+    -9: "FNNUE_E_FEN", -10: "FNNUE_E_CAPACITY", -11: "FNNUE_E_TIMEOUT",
 }
 SYNTH_LEB128, SYNTH_WRAP, SYNTH_FC1_PAD = 1, 2, 4
 GROUP_CHAIN, GROUP_STAR = 0, 1
@@ -138,6 +138,7 @@ SIGNATURES = {
     "fnnue_backend_free": ([_vp], None),
     "fnnue_backend_batch_size": ([_vp, _P(_sz)], _i32),
     "fnnue_backend_go": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp], _i32),
+    "fnnue_backend_go_timeout": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp, _u32], _i32),
     "fnnue_backend_analysis_json": ([_vp, _sz, C.c_char_p, _sz, _P(_sz)], _i32),
     "fnnue_backend_last_stats": ([_vp, _vp], _i32),
 }

@@ -14,6 +14,7 @@ positions) and returns, per batch, its responses or a ``PositionFailed``.
 from __future__ import annotations
 
 import ctypes as C
+import time
 from dataclasses import dataclass, field
 from typing import Sequence
 
@@ -26,7 +27,7 @@ SCORE_CP, SCORE_MATE = 0, 1
 
 
 class _Init(C.Structure):
-    _fields_ = [("normalize_to_pawn", C.c_int32), ("reserved", C.c_uint32)]
+    _fields_ = [("normalize_to_pawn", C.c_int32), ("timeout_ms", C.c_uint32)]
 
 
 class _Acquired(C.Structure):
@@ -130,7 +131,12 @@ class GpuEvalStub:
     def __init__(self, actor: GpuEvalActor):
         self._actor = actor
 
-    def go(self, bodies: Sequence[AcquireResponseBody]) -> list[list[PositionResponse] | PositionFailed]:
+    def go(self, bodies: Sequence[AcquireResponseBody],
+           timeout_ms: int = 0) -> list[list[PositionResponse] | PositionFailed]:
+        """One go() over whole batches, within `timeout_ms` (0: the channel's
+        budget).  A call that overruns it raises FnnueError FNNUE_E_TIMEOUT and
+        breaks the channel (fnnue_backend_go_timeout); `last_batch_rc` then
+        says which batches had been answered."""
         nb = len(bodies)
         if nb == 0:
             return []
@@ -142,7 +148,11 @@ class GpuEvalStub:
         out = (_Response * max(1, cap))()
         off = np.zeros(nb + 1, dtype=np.uint32)
         rc = np.zeros(nb, dtype=np.int32)
-        N.check(N.lib.fnnue_backend_go(self._actor._h, a, nb, out, cap, N.ptr(off), N.ptr(rc)))
+        self.last_batch_rc = rc
+        t0 = time.perf_counter()
+        ret = N.lib.fnnue_backend_go_timeout(self._actor._h, a, nb, out, cap, N.ptr(off), N.ptr(rc), int(timeout_ms))
+        self.last_call_s = time.perf_counter() - t0  # the C call alone (not the ctypes marshalling around it)
+        N.check(ret)
         res: list[list[PositionResponse] | PositionFailed] = []
         for i, b in enumerate(bodies):
             if rc[i]:
@@ -187,12 +197,13 @@ class _Nets(C.Structure):
 
 
 def channel(net=None, device: int = 0, normalize_to_pawn: int = 0, *, crazyhouse=None,
-            atomic=None) -> tuple[GpuEvalStub, GpuEvalActor]:
+            atomic=None, timeout_ms: int = 0) -> tuple[GpuEvalStub, GpuEvalActor]:
     """stockfish::channel for the GPU evaluator.  `net` (a fishnet_amd.Net)
     goes to the slot of its variant; `crazyhouse` / `atomic` add variant nets
-    (fnnue_backend_channel_nets): each batch is evaluated by its variant's net."""
+    (fnnue_backend_channel_nets): each batch is evaluated by its variant's net.
+    `timeout_ms`: the budget of each go() (0: 60 s, [ref] src/main.rs:316)."""
     h = C.c_void_p()
-    init = _Init(normalize_to_pawn, 0)
+    init = _Init(normalize_to_pawn, timeout_ms)
     if crazyhouse is None and atomic is None:
         N.check(N.lib.fnnue_backend_channel(net._h, device, C.byref(init), C.byref(h)))
     else:

@@ -55,6 +55,12 @@ namespace {
 
 constexpr int32_t kNormalizeToPawnSf151 = 361;  // upstream uci.h NormalizeToPawnValue (SF 15.1, recalled)
 constexpr int kKinds = 3;                       // net slots: kVariantChess, kVariantCrazyhouse, kVariantAtomic
+constexpr uint32_t kDefaultTimeoutMs = 60000;
+// Per-batch text bounds: far beyond any lichess batch (a FEN is < 100 bytes;
+// the longest possible game, ~5,900 moves, < 64 KB of UCI), so that a piece's
+// text fits its 32-bit offsets whatever the caller sends.
+constexpr size_t kMaxFenBytes = 4096, kMaxMovesBytes = (size_t)1 << 22;
+constexpr size_t kMaxPieceText = (size_t)1 << 30;  // a new piece before a piece's text passes this   // the worker's budget cap, min(60 s, budget) ([ref] src/main.rs:316)
 using Clock = std::chrono::steady_clock;
 
 double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
@@ -67,6 +73,7 @@ struct Job {
   size_t cap = 0;
   uint32_t* off = nullptr;
   int32_t* rc = nullptr;
+  uint32_t timeout_ms = 0;  // the call's budget (0: the channel's)
   int ret = 0;
   std::string err;  // fnnue_last_error of a failed call
 };
@@ -293,7 +300,7 @@ struct NetWork {
   size_t next = 0;                // first piece whose responses are not written yet
   std::vector<hipEvent_t> ev_done;  // per piece: results and error word on the host
   DevBuf dev, pos;
-  PinnedBuf up, down;
+  PinnedBuf up, down, scratch;      // scratch: a failing piece's positions, read back by recover()
   void clear() {
     games.clear();
     roots.clear();
@@ -319,6 +326,7 @@ struct NetWork {
     pos.release();
     up.release();
     down.release();
+    scratch.release();
     for (hipEvent_t e : ev_done) (void)hipEventDestroy(e);
     ev_done.clear();
   }
@@ -344,6 +352,15 @@ int usable_cpus() {
 
 }  // namespace
 
+struct fnnue_backend;
+namespace {
+// Backends freed while a timed-out call's work was still on their streams
+// (fnnue_backend_free): released here once the streams have drained.
+std::mutex g_abandoned_mu;
+std::vector<fnnue_backend*> g_abandoned;
+void reap_abandoned();
+}  // namespace
+
 struct fnnue_backend {
   fnnue_ctx* ctx[kKinds] = {};  // one evaluator per net, all on one device
   int device = 0;
@@ -354,6 +371,16 @@ struct fnnue_backend {
   size_t fill_grain = 64;        // FNNUE_BACKEND_FILL_GRAIN: games per fill task
   size_t size_grain = 256;       // FNNUE_BACKEND_SIZE_GRAIN: batches per sizing task
   size_t stage_grain = 512;      // FNNUE_BACKEND_STAGE_GRAIN: games per text-staging task
+  // The worker's time budget ([ref] src/main.rs:316, 343-351: a go() that
+  // overruns it fails, and the engine is dropped — its child killed,
+  // stockfish.rs:138).  Every wait of a go() is bounded by the call's
+  // deadline; a call that overruns it returns FNNUE_E_TIMEOUT and breaks the
+  // channel: the device may still be working on the call's pieces (in the
+  // channel's buffers), so later calls fail fast and the caller opens a new
+  // channel, as the worker restarts its engine.
+  uint32_t timeout_ms = kDefaultTimeoutMs;
+  bool broken = false;
+  Clock::time_point deadline;
   // The capacity-1 channel: a go() runs on its caller's thread holding run_mu,
   // so a second caller waits until the first call is answered
   // (mpsc::channel(1) with one message in flight, without a thread hand-off
@@ -386,6 +413,18 @@ struct fnnue_backend {
   }
 
   void run(Job& j);
+  void release_device() {
+    for (NetWork& W : net) W.release();
+    for (fnnue_ctx*& c : ctx) {
+      fnnue_ctx_free(c);
+      c = nullptr;
+    }
+  }
+  bool expired() const { return Clock::now() >= deadline; }
+  int timed_out(const char* where);
+  int wait_event(hipEvent_t e, const char* what);
+  bool streams_idle();
+  void abandon_unanswered(Job& j);
   int prepare_moves(Job& j, int k);
   void layout(const Job& j, int k, Piece& P);
   int plan(Job& j, int k);
@@ -396,6 +435,49 @@ struct fnnue_backend {
   void fill(Job& j, int k, const Piece& P);
   void fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint32_t nps);
 };
+
+int fnnue_backend::timed_out(const char* where) {
+  return fail(FNNUE_E_TIMEOUT, std::string("go() overran its budget of ") + std::to_string(timeout_ms) +
+                                   " ms (" + where + ", " + std::to_string(ms_since(t0)) + " ms in)");
+}
+
+// Waits for an event until the call's deadline: a few microseconds of
+// spinning (a small call's piece is back within them), then the CPU is
+// yielded between polls, so that a long wait does not hold a core the worker
+// threads or the rest of fishnet could use.
+int fnnue_backend::wait_event(hipEvent_t e, const char* what) {
+  for (uint32_t i = 0;; ++i) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return FNNUE_OK;
+    if (q != hipErrorNotReady) return hip_fail(q, what);
+    if (expired()) return timed_out(what);
+    if (i < 512) {
+      for (int p = 0; p < 16; ++p) _mm_pause();
+    } else {
+      sched_yield();
+    }
+  }
+}
+
+// Nothing of the channel's is left on the device (its streams are drained).
+bool fnnue_backend::streams_idle() {
+  for (fnnue_ctx* c : ctx)
+    if (c && hipStreamQuery(c->stream) == hipErrorNotReady) return false;
+  return true;
+}
+
+// After a timeout: the batches whose responses were not written fail with
+// FNNUE_E_TIMEOUT (those already written stand); the channel is broken.
+void fnnue_backend::abandon_unanswered(Job& j) {
+  for (NetWork& W : net) {
+    for (size_t pi = W.next; pi < W.pieces.size(); ++pi)
+      for (size_t i : W.pieces[pi].games) j.rc[i] = FNNUE_E_TIMEOUT;
+    if (W.next < W.pieces.size())  // the move work rides in the net's last piece
+      for (size_t i : W.roots) j.rc[i] = FNNUE_E_TIMEOUT;
+    for (size_t i : W.terminal) j.rc[i] = FNNUE_E_TIMEOUT;
+  }
+  broken = true;
+}
 
 // Move batches of one net, host side: the position after all moves (one per
 // batch) and its legal children with their game-end flags.  A batch whose
@@ -468,14 +550,17 @@ void fnnue_backend::layout(const Job& j, int k, Piece& P) {
 int fnnue_backend::plan(Job& j, int k) {
   NetWork& W = net[k];
   W.pieces.clear();
-  size_t acc = 0, plies = 0;
+  size_t acc = 0, plies = 0, text = 0;
   for (size_t i : W.games) {
-    if (W.pieces.empty() || acc >= piece_plies) {
+    const size_t t = (size_t)flen[i] + 1 + mlen[i];
+    if (W.pieces.empty() || acc >= piece_plies || text + t > kMaxPieceText) {
       W.pieces.emplace_back();
       acc = 0;
+      text = 0;
     }
     W.pieces.back().games.push_back(i);
     acc += j.off[i + 1] - j.off[i];
+    text += t;
     plies += j.off[i + 1] - j.off[i];
   }
   if (plies >= (1ull << 31)) return fail(FNNUE_E_ARG, "batch too large");
@@ -618,9 +703,10 @@ int fnnue_backend::finish(Job& j, int k, bool wait, bool* ready) {
   if (wait) {
     const auto tw = Clock::now();
     mark("wait", k, (long)pi);
-    HIP_TRY(hipEventSynchronize(W.ev_done[pi]), "hipEventSynchronize");
+    const int rc = wait_event(W.ev_done[pi], "waiting for a piece's results");
     wait_ms += ms_since(tw);
     ++syncs;
+    if (rc) return rc;
   } else {
     const hipError_t q = hipEventQuery(W.ev_done[pi]);
     if (q == hipErrorNotReady) return FNNUE_OK;
@@ -648,28 +734,50 @@ int fnnue_backend::recover(Job& j, int k, size_t pi) {
     const uint32_t cerr = berr[3];
     if (!berr[0] && !cerr) break;
     if (berr[0]) {
-      // The builder names the failing game; that batch fails (PositionFailed)
-      // and the rest are staged again.  A count mismatch or a game index
-      // outside the piece cannot be blamed on any batch: the call fails.
-      if (berr[0] == kBuildErrCount || berr[1] >= P.ng)
-        return fail(FNNUE_E_DEVICE, "batch builder reported game " + std::to_string(berr[1]) + " of " +
-                                        std::to_string(P.ng) + " (code " + std::to_string(berr[0]) + ")");
-      j.rc[P.games[berr[1]]] = berr[0] == kBuildErrFen ? FNNUE_E_FEN : FNNUE_E_MOVE;
-      P.games.erase(P.games.begin() + berr[1]);
+      // The replay flags every game it rejected (kFinalFailed | code in the
+      // game's flag byte); those batches fail (PositionFailed) and the rest
+      // are staged again, in one pass however many failed.  A count mismatch
+      // or a game index outside the piece cannot be blamed on any batch: the
+      // call fails.
+      auto bad_word = [&](uint32_t code, uint32_t g) {
+        return fail(FNNUE_E_DEVICE, "batch builder reported game " + std::to_string(g) + " of " +
+                                        std::to_string(P.ng) + " (code " + std::to_string(code) + ")");
+      };
+      if (berr[0] == kBuildErrCount || berr[1] >= P.ng) return bad_word(berr[0], berr[1]);
+      const uint8_t* fin = W.down.at<uint8_t>(P.down0) + (P.o_fin - P.o_res);
+      std::vector<size_t> keep;
+      keep.reserve(P.games.size());
+      for (uint32_t g = 0; g < P.ng; ++g) {
+        const uint32_t code = fin[g] & kFinalFailed ? fin[g] & ~kFinalFailed & 0xFFu : 0u;
+        if (code == kBuildErrCount || code > kBuildErrCount) return bad_word(code, g);
+        if (code)
+          j.rc[P.games[g]] = code == kBuildErrFen ? FNNUE_E_FEN : FNNUE_E_MOVE;
+        else
+          keep.push_back(P.games[g]);
+      }
+      if (keep.size() == P.games.size()) return bad_word(berr[0], berr[1]);  // the named game carries no flag
+      P.games.swap(keep);
     } else {
       // A FEN the builder parses but the evaluator cannot (kings, > 32
       // pieces): find the games holding such positions, fail those batches.
       // (Move-work children were checked on the host.)
-      std::vector<uint8_t> hpos((size_t)P.n * W.rec);
-      if (!hpos.empty())
-        HIP_TRY(hipMemcpy(hpos.data(), W.pos.at<char>(P.pos0), hpos.size(), hipMemcpyDeviceToHost), "D2H(positions)");
+      const size_t nbytes = (size_t)P.n * W.rec;
+      if (int rc = W.scratch.reserve(nbytes + 1)) return rc;
+      const uint8_t* hpos = W.scratch.at<uint8_t>(0);
+      if (nbytes) {
+        hipStream_t s = ctx[k]->stream;
+        HIP_TRY(hipMemcpyAsync(W.scratch.p, W.pos.at<char>(P.pos0), nbytes, hipMemcpyDeviceToHost, s),
+                "D2H(positions)");
+        HIP_TRY(hipEventRecord(W.ev_done[pi], s), "hipEventRecord(positions)");
+        if (int rc = wait_event(W.ev_done[pi], "reading a failing piece's positions")) return rc;
+      }
       ++syncs;
       const uint32_t* ply = W.up.at<uint32_t>(P.up0 + P.o_ply);
       std::vector<size_t> keep;
       for (uint32_t g = 0; g < P.ng; ++g) {
         bool ok = true;
         for (uint32_t x = ply[g]; x < ply[g + 1] && ok; ++x) {
-          const uint8_t* p = hpos.data() + (size_t)x * W.rec;
+          const uint8_t* p = hpos + (size_t)x * W.rec;
           ok = k == kVariantChess ? valid_host_pos(*reinterpret_cast<const fnnue_pos*>(p))
                                   : host_vpos_state(*reinterpret_cast<const fnnue_vpos*>(p), k) != 0;
         }
@@ -690,8 +798,9 @@ int fnnue_backend::recover(Job& j, int k, size_t pi) {
     layout(j, k, P);  // fewer games: the piece still fits its place
     if (int rc = stage_up(j, k, pi)) return rc;
     if (int rc = stage_eval(k, pi)) return rc;
-    HIP_TRY(hipEventSynchronize(W.ev_done[pi]), "hipEventSynchronize");
+    const int rc = wait_event(W.ev_done[pi], "waiting for a restaged piece");
     ++syncs;
+    if (rc) return rc;
     P.pending = false;
   }
   return FNNUE_OK;
@@ -808,6 +917,7 @@ void fnnue_backend::fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint3
 
 void fnnue_backend::run(Job& j) {
   t0 = Clock::now();
+  deadline = t0 + std::chrono::milliseconds(j.timeout_ms ? j.timeout_ms : timeout_ms);
   tl.clear();
   filled = 0;
   fill_ms = wait_ms = 0;
@@ -838,8 +948,14 @@ void fnnue_backend::run(Job& j) {
       } else {
         n = (uint32_t)(a.moves ? scan_tokens(a.moves, &ml) : 0) + 1;
       }
-      flen[i] = (uint32_t)std::min<size_t>(fl, 1u << 30);
-      mlen[i] = (uint32_t)std::min<size_t>(ml, 1u << 30);
+      // text beyond any real batch fails that batch alone (it
+      // used to be clamped, failing the whole call later)
+      if (rc == FNNUE_OK && (fl > kMaxFenBytes || ml > kMaxMovesBytes)) {
+        rc = FNNUE_E_ARG;
+        fl = ml = 0;
+      }
+      flen[i] = (uint32_t)fl;
+      mlen[i] = (uint32_t)ml;
       const int kd = kind_of(a.variant);
       if (rc == FNNUE_OK && (kd < 0 || !ctx[kd])) rc = FNNUE_E_ARCH;  // no net for this variant on this backend
       if (rc == FNNUE_OK && a.multipv < 0) rc = FNNUE_E_ARG;
@@ -851,7 +967,16 @@ void fnnue_backend::run(Job& j) {
   });
   mark("sizes");
   j.off[0] = 0;
-  for (size_t i = 0; i < nb; ++i) j.off[i + 1] += j.off[i];
+  uint64_t total = 0;
+  for (size_t i = 0; i < nb; ++i) {
+    total += j.off[i + 1];
+    j.off[i + 1] = (uint32_t)total;
+  }
+  if (total > UINT32_MAX) {  // the offsets are 32-bit
+    j.ret = fail(FNNUE_E_ARG, "the batches expand to " + std::to_string(total) + " responses, more than 2^32 - 1");
+    j.err = g_err;
+    return;
+  }
   if (j.off[nb] > j.cap) {
     j.ret = fail(FNNUE_E_CAPACITY, "response buffer holds " + std::to_string(j.cap) + ", batches need " +
                                        std::to_string(j.off[nb]));
@@ -895,6 +1020,7 @@ void fnnue_backend::run(Job& j) {
     if (rc == FNNUE_OK && (!W.games.empty() || W.nk)) rc = plan(j, k);
     rounds = std::max(rounds, W.pieces.size());
   }
+  if (rc == FNNUE_OK && expired()) rc = timed_out("sizing and planning");
   mark("planned");
   // Enqueue order: every net's first upload + replay (the nets' streams run
   // side by side), then each round's evaluations behind the next round's
@@ -911,6 +1037,10 @@ void fnnue_backend::run(Job& j) {
     return FNNUE_OK;
   };
   for (size_t r = 0; r <= rounds && rc == FNNUE_OK; ++r) {
+    if (r && expired()) {
+      rc = timed_out("staging pieces");
+      break;
+    }
     for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k)
       if (r < net[k].pieces.size()) rc = stage_up(j, k, r);
     for (int k = 0; k < kKinds && rc == FNNUE_OK; ++k)
@@ -921,6 +1051,7 @@ void fnnue_backend::run(Job& j) {
   // back are written while another net's are still on the device (the small
   // variant nets' usually are back first); the host blocks only when a
   // single net is left.
+  uint32_t idle_polls = 0;
   while (rc == FNNUE_OK) {
     bool progress = false;
     int first = -1, left = 0;
@@ -942,11 +1073,27 @@ void fnnue_backend::run(Job& j) {
     if (left == 1 || !any_order) {
       bool ready = false;
       rc = finish(j, first, true, &ready);
-    } else {  // polling counts as waiting for the device
+    } else {  // polling counts as waiting for the device; a long wait yields the CPU
       const auto tw = Clock::now();
-      for (int i = 0; i < 64; ++i) _mm_pause();
+      if (++idle_polls < 256) {
+        for (int i = 0; i < 64; ++i) _mm_pause();
+      } else {
+        sched_yield();
+      }
       wait_ms += ms_since(tw);
+      if (expired()) rc = timed_out("waiting for the nets' pieces");
     }
+    if (progress) idle_polls = 0;
+  }
+  if (rc == FNNUE_E_TIMEOUT) {
+    // The device may still be running this call's pieces, which read and
+    // write the channel's pinned buffers: nothing waits for them; the channel
+    // is broken (later calls fail fast, fnnue_backend_free reclaims the
+    // buffers once the streams have drained).
+    abandon_unanswered(j);
+    j.ret = rc;
+    j.err = g_err;
+    return;
   }
   if (rc) {
     for (int k = 0; k < kKinds; ++k) {  // the pinned images stay in use until the copies are done
@@ -996,6 +1143,31 @@ void fnnue_backend::run(Job& j) {
   stats.pieces = npieces;
 }
 
+namespace {
+void reap_abandoned() {
+  std::vector<fnnue_backend*> done;
+  {
+    std::lock_guard<std::mutex> lk(g_abandoned_mu);
+    for (size_t i = 0; i < g_abandoned.size();) {
+      fnnue_backend* b = g_abandoned[i];
+      DeviceGuard g(b->device);
+      if (b->streams_idle()) {
+        done.push_back(b);
+        g_abandoned[i] = g_abandoned.back();
+        g_abandoned.pop_back();
+      } else {
+        ++i;
+      }
+    }
+  }
+  for (fnnue_backend* b : done) {
+    DeviceGuard g(b->device);
+    b->release_device();
+    delete b;
+  }
+}
+}  // namespace
+
 extern "C" {
 
 int fnnue_backend_batch_size(const fnnue_acquired* a, size_t* n) {
@@ -1025,6 +1197,7 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
     if (variant != k) return fail(FNNUE_E_ARCH, std::string("the ") + kName[k] + " slot needs a " + kName[k] + " net");
   }
   if (init && init->normalize_to_pawn < 0) return fail(FNNUE_E_ARG, "normalize_to_pawn must be positive");
+  reap_abandoned();
   fnnue_backend* b = nullptr;
   try {
     b = new fnnue_backend();
@@ -1033,6 +1206,7 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets* nets, int device, const
   }
   b->device = device;
   if (init && init->normalize_to_pawn > 0) b->norm = init->normalize_to_pawn;
+  if (init && init->timeout_ms > 0) b->timeout_ms = init->timeout_ms;
   {
     // host threads for the text staging and response fill of large calls: up
     // to 8, at most the CPUs this process may run on (12 or 16: within the
@@ -1089,14 +1263,23 @@ void fnnue_backend_free(fnnue_backend* b) {
   b->pool.stop();
   {
     DeviceGuard g(b->device);
-    for (NetWork& W : b->net) W.release();
+    if (b->broken && !b->streams_idle()) {
+      // A timed-out call's pieces are still on the device: freeing their
+      // buffers (or the contexts) would wait for them.  The backend is parked
+      // and released by a later channel() / free() once its streams drain.
+      std::lock_guard<std::mutex> lk(g_abandoned_mu);
+      g_abandoned.push_back(b);
+      return;
+    }
+    b->release_device();
   }
-  for (fnnue_ctx* c : b->ctx) fnnue_ctx_free(c);
   delete b;
+  reap_abandoned();
 }
 
-int fnnue_backend_go(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches, fnnue_position_response* out,
-                     size_t cap, uint32_t* off, int32_t* batch_rc) {
+int fnnue_backend_go_timeout(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches,
+                             fnnue_position_response* out, size_t cap, uint32_t* off, int32_t* batch_rc,
+                             uint32_t timeout_ms) {
   if (!b || !off || !batch_rc || (nbatches && !batches) || (cap && !out)) return fail(FNNUE_E_ARG, "null argument");
   if (nbatches > (1u << 24)) return fail(FNNUE_E_ARG, "too many batches");
   Job j;
@@ -1106,13 +1289,23 @@ int fnnue_backend_go(fnnue_backend* b, const fnnue_acquired* batches, size_t nba
   j.cap = cap;
   j.off = off;
   j.rc = batch_rc;
+  j.timeout_ms = timeout_ms;
   std::lock_guard<std::mutex> lk(b->run_mu);  // mpsc::Sender::send on a full channel waits
   if (b->closed) return fail(FNNUE_E_DEVICE, "backend actor stopped");
+  if (b->broken) {
+    for (size_t i = 0; i < nbatches; ++i) batch_rc[i] = FNNUE_E_TIMEOUT;
+    return fail(FNNUE_E_TIMEOUT, "the channel is broken: an earlier go() overran its budget (open a new channel)");
+  }
   DeviceGuard g(b->device);
   g_err.clear();
   b->run(j);
   if (j.ret) return fail(j.ret, j.err);
   return FNNUE_OK;
+}
+
+int fnnue_backend_go(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches, fnnue_position_response* out,
+                     size_t cap, uint32_t* off, int32_t* batch_rc) {
+  return fnnue_backend_go_timeout(b, batches, nbatches, out, cap, off, batch_rc, 0);
 }
 
 int fnnue_backend_last_stats(fnnue_backend* b, fnnue_backend_stats* out) {

@@ -40,6 +40,8 @@ constexpr uint32_t kBuildErrFen = 1, kBuildErrMove = 2, kBuildErrCount = 3;
 // (checkmated, or atomic: its king exploded) or `score cp 0` (stalemate)
 // ([ref] src/stockfish.rs:359-376 parses them to Score::Mate(0) / Cp(0)).
 constexpr uint8_t kFinalNoMoves = 1, kFinalCheck = 2, kFinalExtinct = 4;
+// A game the replay rejected: kFinalFailed | its kBuildErr* code (replay_games_device).
+constexpr uint8_t kFinalFailed = 0x80;
 
 struct BuildResult {
   hipError_t hip = hipSuccess;

@@ -101,6 +101,14 @@ __device__ __forceinline__ void latch(uint32_t* err, uint32_t code, uint32_t gam
   }
 }
 
+// A failing game: the error word names the first one (err[0..2]); the game's
+// own flag byte says that it failed and why (kFinalFailed | code), so that a
+// caller drops every failing game of a launch in one pass.
+__device__ __forceinline__ void fail_game(uint32_t* err, uint8_t* final, uint32_t code, uint32_t game, uint32_t ply) {
+  latch(err, code, game, ply);
+  if (final) final[game] = (uint8_t)(kFinalFailed | code);
+}
+
 constexpr int kTokRing = 128;  // pending move codes (<= 63 left + 32 new per 64 characters)
 constexpr int kTxt = 2048;     // move text staged in LDS at a time
 
@@ -382,13 +390,13 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   const uint32_t f0 = fen_off[g], m0 = mv_off[g], e = fen_off[g + 1];
   const uint32_t o0 = ply_off[g], nply = ply_off[g + 1] - o0;
   if (nply == 0) {
-    if (lane == 0) latch(err, kBuildErrCount, g, 0);
+    if (lane == 0) fail_game(err, final, kBuildErrCount, g, 0);
     return;
   }
   const uint32_t nmoves = nply - 1;
   Board root;
   if (!root_board<R>(variant, text, f0, m0, TXT, lane, root)) {
-    if (lane == 0) latch(err, kBuildErrFen, g, 0);
+    if (lane == 0) fail_game(err, final, kBuildErrFen, g, 0);
     return;
   }
   if (lane == 0) {
@@ -428,7 +436,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
     bad_ply = nmoves + 1;
   }
   if (bad) {
-    if (lane == 0) latch(err, bad, g, bad_ply);
+    if (lane == 0) fail_game(err, final, bad, g, bad_ply);
     return;
   }
   if (final) {
@@ -461,7 +469,11 @@ struct PairLds {
   uint32_t KW[2], KP[2];        // codes, moves played
   uint32_t TK[kTokRing];        // the tokeniser's ring
   uint32_t FIN[16];             // the last board's bytes
-  uint32_t nw, cnt_ply, bad, bad_ply;
+  // Control words (windows, count error ply, bad-move code and ply), double
+  // buffered by barrier: the copy written before barrier m is slot m & 1,
+  // read by both waves right after it; the next writes go to the other slot,
+  // so a wave that runs ahead never overwrites what the other still reads.
+  uint32_t CTL[2][4];
   char TXT[kTxt];
 };
 
@@ -486,11 +498,25 @@ __global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const cha
   const uint32_t f0 = fen_off[g], m0 = mv_off[g], e = fen_off[g + 1];
   const uint32_t o0 = ply_off[g], nply = ply_off[g + 1] - o0;
   if (nply == 0) {
-    if (threadIdx.x == 0) latch(err, kBuildErrCount, g, 0);
+    if (threadIdx.x == 0) fail_game(err, final, kBuildErrCount, g, 0);
     return;
   }
   const uint32_t nmoves = nply - 1;
   const uint32_t nw0 = (nmoves + 63) / 64;
+  // the control words in registers (wave-uniform): reloaded after every barrier
+  uint32_t nw = nw0, cnt_ply = 0, bad = 0, bad_ply = 0;
+  auto publish = [&](int slot) {  // lane 0 of the writing wave
+    L.CTL[slot][0] = nw;
+    L.CTL[slot][1] = cnt_ply;
+    L.CTL[slot][2] = bad;
+    L.CTL[slot][3] = bad_ply;
+  };
+  auto reload = [&](int slot) {
+    nw = L.CTL[slot][0];
+    cnt_ply = L.CTL[slot][1];
+    bad = L.CTL[slot][2];
+    bad_ply = L.CTL[slot][3];
+  };
   // wave 0: the root; wave 1 waits (the FEN goes through TXT, which wave 1
   // then uses for the move text)
   Sc sc;
@@ -499,10 +525,8 @@ __global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const cha
     Board root;
     const bool ok = root_board<R>(variant, text, f0, m0, L.TXT, lane, root);
     if (lane == 0) {
-      L.bad = ok ? 0u : kBuildErrFen;
-      L.bad_ply = 0;
-      L.cnt_ply = 0;
-      L.nw = nw0;
+      bad = ok ? 0u : kBuildErrFen;
+      publish(0);  // barrier 0
       if (ok && out) out[o0] = R::pack(root);
       if (ok && states) states[o0] = root;
     }
@@ -512,8 +536,9 @@ __global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const cha
     }
   }
   __syncthreads();
-  if (L.bad) {
-    if (threadIdx.x == 0) latch(err, L.bad, g, 0);
+  reload(0);
+  if (bad) {
+    if (threadIdx.x == 0) fail_game(err, final, bad, g, 0);
     return;
   }
   // wave 1: the codes of window w (k = its moves, fewer when the text ends:
@@ -527,20 +552,22 @@ __global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const cha
     lds_fence();
     if (lane == 0) L.KW[w & 1] = got;
     if (got < need) {  // the text ended: this window is the game's last
-      if (lane == 0) {
-        L.cnt_ply = 64 * w + got + 1;
-        L.nw = w + 1;
-      }
+      cnt_ply = 64 * w + got + 1;
+      nw = w + 1;
     } else {
       tok_consume(t, L.TK, got, lane);
-      if (w + 1 == nw0 && tok_extra(t, text, e, lane) && lane == 0) L.cnt_ply = nmoves + 1;
+      if (w + 1 == nw0 && tok_extra(t, text, e, lane)) cnt_ply = nmoves + 1;
     }
   };
-  if (wv == 1 && nw0 > 0) produce(0);
+  if (wv == 1) {
+    if (nw0 > 0) produce(0);
+    if (lane == 0) publish(1);  // barrier 1
+  }
   __syncthreads();
+  reload(1);
   uint8_t fl = 0;
   for (uint32_t s = 0;; ++s) {
-    const uint32_t nw = L.nw;
+    // nw (as of this iteration's barrier) is the same in both waves
     if (wv == 0) {
       if (s < nw) {
         const uint32_t b = s & 1, k = L.KW[b];
@@ -571,7 +598,8 @@ __global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const cha
         fl = final_flags<R>(L.FIN, sc, lane);
       }
     } else {
-      if (s >= 1 && s - 1 < nw) {
+      const uint32_t nw_s = nw;
+      if (s >= 1 && s - 1 < nw_s) {
         const uint32_t w0 = s - 1, b = w0 & 1, k = L.KW[b], kplay = L.KP[b];
         Sc sc0;
         uint32_t sw[kScw];
@@ -588,19 +616,21 @@ __global__ __launch_bounds__(128) void replay_pair_kernel(int variant, const cha
         for (int w = 0; w < R::kVary; ++w) scw[w] = L.SCW[b][w][lane];
         const uint32_t first = check<R>(sc0, win, L.SNAP[b], kplay, k, L.MV[b][lane], scw, lane, out, states,
                                         o0 + 64 * w0 + 1);
-        if (first < k && lane == 0) {
-          L.bad = kBuildErrMove;
-          L.bad_ply = 64 * w0 + first + 1;
+        if (first < k) {
+          bad = kBuildErrMove;
+          bad_ply = 64 * w0 + first + 1;
         }
       }
-      if (s + 1 < nw) produce(s + 1);
+      if (s + 1 < nw_s) produce(s + 1);
+      if (lane == 0) publish((int)(s & 1));  // barrier s + 2
     }
     __syncthreads();
-    if (L.bad || s >= L.nw) break;
+    reload((int)(s & 1));
+    if (bad || s >= nw) break;
   }
   if (threadIdx.x == 0) {
-    if (L.bad) latch(err, L.bad, g, L.bad_ply);
-    else if (L.cnt_ply) latch(err, kBuildErrCount, g, L.cnt_ply);
+    if (bad) fail_game(err, final, bad, g, bad_ply);
+    else if (cnt_ply) fail_game(err, final, kBuildErrCount, g, cnt_ply);
     else if (final) final[g] = fl;
   }
 }

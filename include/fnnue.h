@@ -50,6 +50,7 @@ extern "C" {
 #define FNNUE_E_MOVE (-8)       /* illegal or unparsable UCI move                      */
 #define FNNUE_E_FEN (-9)        /* unparsable FEN                                      */
 #define FNNUE_E_CAPACITY (-10)  /* output buffer too small                             */
+#define FNNUE_E_TIMEOUT (-11)   /* fnnue_backend_go overran its time budget           */
 
 typedef struct fnnue_net fnnue_net; /* parsed, validated, immutable host copy of a .nnue */
 typedef struct fnnue_ctx fnnue_ctx; /* one GPU: device-resident net + workspaces          */

@@ -72,7 +72,8 @@ typedef struct fnnue_backend fnnue_backend;
 /* StockfishInit (stockfish.rs): what the engine is configured with. */
 typedef struct {
   int32_t normalize_to_pawn; /* cp = v * 100 / normalize_to_pawn; 0 -> 361 */
-  uint32_t reserved;
+  uint32_t timeout_ms;       /* budget of one go(): 0 -> 60000, the worker's cap min(60 s, budget)
+                                ([ref] src/main.rs:316); see fnnue_backend_go_timeout */
 } fnnue_backend_init;
 
 /* AcquireResponseBody (api.rs:293-309) of one batch. */
@@ -122,7 +123,10 @@ int fnnue_backend_channel_nets(const fnnue_backend_nets *nets, int device, const
                                fnnue_backend **out);
 /* The one-net form: the net goes to the slot of its variant. */
 int fnnue_backend_channel(const fnnue_net *net, int device, const fnnue_backend_init *init, fnnue_backend **out);
-/* Stops the actor (after the call in flight) and frees it. */
+/* Stops the actor (after the call in flight) and frees it.  Never waits for
+ * the device: when a timed-out call's work is still running on the channel's
+ * streams, its buffers are released later (by a later channel() or free()),
+ * once the streams have drained. */
 void fnnue_backend_free(fnnue_backend *b);
 
 /* Number of responses batch `a` expands to (IncomingBatch::from_acquired):
@@ -136,6 +140,21 @@ int fnnue_backend_batch_size(const fnnue_acquired *a, size_t *n);
  * Thread-safe: concurrent callers queue on the capacity-1 channel. */
 int fnnue_backend_go(fnnue_backend *b, const fnnue_acquired *batches, size_t nbatches, fnnue_position_response *out,
                      size_t cap, uint32_t *off, int32_t *batch_rc);
+
+/* go() with its own budget (timeout_ms; 0 = the channel's init.timeout_ms).
+ * The reference worker races each go against `min(60 s, budget) +
+ * work.timeout()` and, when it runs out, drops the engine (the child is
+ * killed) and fails the batch ([ref] src/main.rs:316, 343-351;
+ * src/stockfish.rs:138).  Here every wait of the call is bounded by that
+ * deadline; on expiry the call returns FNNUE_E_TIMEOUT at once, without
+ * waiting for the device: batch_rc[i] = 0 for the batches whose responses were
+ * written before the deadline (valid), FNNUE_E_TIMEOUT for the others.  The
+ * channel is then broken — the device may still be working in its buffers —
+ * and every later go() on it fails fast with FNNUE_E_TIMEOUT; free it and open
+ * a new channel (the worker's drop-and-restart). */
+int fnnue_backend_go_timeout(fnnue_backend *b, const fnnue_acquired *batches, size_t nbatches,
+                             fnnue_position_response *out, size_t cap, uint32_t *off, int32_t *batch_rc,
+                             uint32_t timeout_ms);
 
 /* Where the last go() spent its time (diagnostics; the reference's engine
  * reports only time / nps per position).  Each net's games are cut into pieces

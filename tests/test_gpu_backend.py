@@ -297,6 +297,24 @@ def _stm_squares(fen):
     return sq
 
 
+def _go_both_replays(stub, bodies):
+    """One go() over all the bodies (more than 1024 games: one replay wave per
+    game) and the same bodies in go() calls of 1000 (the two-wave replay,
+    ADVICE r05): the same batches fail with the same codes, the others give
+    the same results."""
+    assert len(bodies) > 1024
+    res = stub.go(bodies)
+    for lo in range(0, len(bodies), 1000):
+        part = stub.go(bodies[lo:lo + 1000])
+        for i, (a, r) in enumerate(zip(res[lo:lo + 1000], part)):
+            if isinstance(a, B.PositionFailed):
+                assert isinstance(r, B.PositionFailed) and r.code == a.code, (bodies[lo + i].batch_id, r)
+            else:
+                assert not isinstance(r, B.PositionFailed), (bodies[lo + i].batch_id, r)
+                assert [(x.psqt, x.positional, x.score) for x in a] == [(x.psqt, x.positional, x.score) for x in r]
+    return res
+
+
 def test_every_token_matches_the_host_builder(chan):
     """Every from-square of the side to move x every destination x {none,
     q, n, r, b, k, Q} as a one-move analysis batch: the device replay accepts
@@ -316,7 +334,7 @@ def test_every_token_matches_the_host_builder(chan):
                         pos = None
                     bodies.append(B.AcquireResponseBody(f"{fi}:{tok}", fen, tok))
                     host.append(pos)
-    res = stub.go(bodies)
+    res = _go_both_replays(stub, bodies)
     ok = [i for i, p in enumerate(host) if p is not None]
     assert 200 < len(ok) < len(host)
     for i, (b, r) in enumerate(zip(bodies, res)):
@@ -364,7 +382,7 @@ def test_every_variant_token_matches_the_host_builder(chan):
             bodies.append(B.AcquireResponseBody(f"{fi}:{tok}", fen, tok, variant=vname))
             host.append(p)
             kinds.append(variant)
-    res = stub.go(bodies)
+    res = _go_both_replays(stub, bodies)
     for i, (b, r) in enumerate(zip(bodies, res)):
         assert isinstance(r, B.PositionFailed) == (host[i] is None), (b.batch_id, r)
     for variant in (ZH, AT):
@@ -431,3 +449,125 @@ def test_pieces_with_failures_in_between(monkeypatch):
                 assert [(x.psqt, x.positional, x.score) for x in a] == [(x.psqt, x.positional, x.score) for x in r]
     finally:
         actor.close()
+
+
+def test_move_work_isolation(chan):
+    """move-work roots whose children the evaluator would reject
+    (a chess root with more than 32 pieces; crazyhouse roots whose pockets
+    exceed the feature set's limits) fail their own batches with
+    FNNUE_E_POSITION, checked on the host before anything reaches the device;
+    good analysis and move batches of the same go() are bit-exact
+    ([ref] src/queue.rs:207-213: only the failed batch is dropped)."""
+    stub, on = chan
+    crowded = "rnbqkbnr/pppppppp/pppppppp/8/8/PPPPPPPP/PPPPPPPP/RNBQKBNR w - - 0 1"
+    zh_over = "rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR[QQ] w KQkq - 0 1"       # 34 pieces with the hand
+    zh_pawns = "4k3/8/8/8/8/8/8/4K3[PPPPPPPPPPPPPPPPPPPPP] w - - 0 1"               # 21 pawns of one type in hand
+    g0, g1 = GAMES[5], GAMES[6]
+    mv0 = " ".join(g0["moves"].split()[:24])
+    bodies = [
+        B.AcquireResponseBody("a0", g0["position"], g0["moves"]),
+        B.AcquireResponseBody("bad-crowded", crowded, "", work="move"),
+        B.AcquireResponseBody("m0", g0["position"], mv0, work="move"),
+        B.AcquireResponseBody("bad-zh", zh_over, "", work="move", variant="crazyhouse"),
+        B.AcquireResponseBody("zh-good", ZH_START, "e2e4 d7d5 e4d5", work="move", variant="crazyhouse"),
+        B.AcquireResponseBody("bad-zh-pawns", zh_pawns, "", work="move", variant="crazyhouse"),
+        B.AcquireResponseBody("a1", g1["position"], g1["moves"]),
+        B.AcquireResponseBody("zh-a", ZH_START, F.random_vgame(31, ZH, ZH_START, 50), variant="crazyhouse"),
+    ]
+    res = stub.go(bodies)
+    codes = {b.batch_id: (r.code if isinstance(r, B.PositionFailed) else 0) for b, r in zip(bodies, res)}
+    assert codes == {"a0": 0, "bad-crowded": -6, "m0": 0, "bad-zh": -6, "zh-good": 0, "bad-zh-pawns": -6,
+                     "a1": 0, "zh-a": 0}, codes
+    check_rows(on, bodies[0], res[0])
+    check_rows(on, bodies[6], res[6])
+    check_rows(on, bodies[7], res[7], ZH)
+    for i, variant in ((2, 0), (4, ZH)):
+        (r,) = res[i]
+        kids, ps, po = search1(on, bodies[i].position, bodies[i].moves, variant)
+        vals = [-int((int(a) + int(b)) / 16) for a, b in zip(ps, po)]
+        assert r.nodes == len(kids) and r.score == B.Score("cp", int(max(vals) * 100 / 361)), bodies[i].batch_id
+
+
+def _long_game(seed, plies):
+    moves = F.random_game(seed, START, plies).split()
+    assert len(moves) > 200, len(moves)
+    return moves
+
+
+@pytest.mark.parametrize("fillers", [0, 1100])  # <= 1024 games: the two-wave replay; more: one wave per game
+def test_failures_in_late_replay_windows(chan, fillers):
+    """Illegal moves in the replay's third and fifth 64-move windows (ADVICE
+    r05: the two-wave kernel's double buffers, window count and bad-move
+    report past the first windows) fail exactly their batches; the long good
+    games around them are bit-exact, in both replay kernels."""
+    stub, on = chan
+    good = [_long_game(100 + s, 320) for s in range(3)]
+    bad3 = list(good[0][:150]) + ["b2b2"] + list(good[0][150:])      # window 2 (plies 129-192)
+    bad5 = list(good[1][:270]) + ["a1a1"] + list(good[1][270:])      # window 4 (plies 257-320)
+    short = list(good[2][:200]) + ["zz"]                              # unparsable token in window 3
+    bodies = [B.AcquireResponseBody("g0", START, " ".join(good[0])),
+              B.AcquireResponseBody("bad3", START, " ".join(bad3)),
+              B.AcquireResponseBody("g1", START, " ".join(good[1])),
+              B.AcquireResponseBody("bad5", START, " ".join(bad5)),
+              B.AcquireResponseBody("g2", START, " ".join(good[2])),
+              B.AcquireResponseBody("short", START, " ".join(short))]
+    bodies += [B.AcquireResponseBody(f"f{i}", START, "e2e4 e7e5" if i % 2 else "d2d4") for i in range(fillers)]
+    res = stub.go(bodies)
+    # the three rejected games are dropped in one extra pass (each game's flag
+    # byte says it failed), not one pass per failure (ADVICE r05)
+    assert B.last_stats(stub._actor)["rebuilds"] == 1
+    for b, r in zip(bodies, res):
+        if b.batch_id in ("bad3", "bad5", "short"):
+            assert isinstance(r, B.PositionFailed) and r.code == -8, (b.batch_id, r)
+        else:
+            assert not isinstance(r, B.PositionFailed), (b.batch_id, r)
+    for i in (0, 2, 4):
+        check_rows(on, bodies[i], res[i])
+    if fillers:
+        check_rows(on, bodies[6], res[6])
+        check_rows(on, bodies[7], res[7])
+
+
+def test_go_timeout_breaks_the_channel():
+    """The worker's time budget ([ref] src/main.rs:316, 343-351; the engine is
+    dropped on expiry, src/stockfish.rs:138): a 16384-batch go() with a 1 ms
+    budget returns FNNUE_E_TIMEOUT well within a second, without waiting for
+    the device; the batches it had not answered say FNNUE_E_TIMEOUT; the next
+    go() on the broken channel fails fast; freeing it does not hang; a new
+    channel on the same device answers bit-exact against the oracle."""
+    import time
+    data = net_bytes(1, 1024, 0)
+    on = {0: OracleNet(data)}
+    bodies = [B.AcquireResponseBody(f"b{i}", GAMES[i % len(GAMES)]["position"], GAMES[i % len(GAMES)]["moves"])
+              for i in range(16384)]
+    stub, actor = B.channel(F.Net.from_bytes(data), 0)
+    try:
+        warm = stub.go(bodies[:64])
+        assert not any(isinstance(r, B.PositionFailed) for r in warm)
+        with pytest.raises(F.FnnueError) as e:
+            stub.go(bodies, timeout_ms=1)
+        assert e.value.name == "FNNUE_E_TIMEOUT", e.value
+        assert stub.last_call_s < 1.0, stub.last_call_s
+        rc = stub.last_batch_rc
+        assert set(np.unique(rc).tolist()) <= {0, -11} and (rc == -11).sum() > 0
+        with pytest.raises(F.FnnueError) as e:
+            stub.go(bodies[:4])
+        assert e.value.name == "FNNUE_E_TIMEOUT" and stub.last_call_s < 0.05
+        assert (stub.last_batch_rc == -11).all()
+    finally:
+        t = time.perf_counter()
+        actor.close()
+        assert time.perf_counter() - t < 5.0
+    stub2, actor2 = B.channel(F.Net.from_bytes(data), 0, timeout_ms=30000)
+    try:
+        res = stub2.go(bodies[:300])
+        for b, rows in zip(bodies[:300], res):
+            assert not isinstance(rows, B.PositionFailed), rows
+        for i in range(0, 300, 7):
+            check_rows(on, bodies[i], res[i])
+        big = stub2.go(bodies)  # the full call within its budget on the new channel
+        assert not any(isinstance(r, B.PositionFailed) for r in big)
+        for i in range(0, 16384, 911):
+            check_rows(on, bodies[i], big[i])
+    finally:
+        actor2.close()
