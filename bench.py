@@ -95,6 +95,8 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=3.0, help="wall budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="default run: skip the extra config-3 and engine-actor lines appended after the headline")
     ap.add_argument("--no-host-api", action="store_true", help="skip timing the host-buffer entry points")
     ap.add_argument("--kernel-events", choices=["ft", "all"], default="ft",
                     help="HIP events in the timed steps: around the FT main kernel only (default), or around every "
@@ -286,7 +288,48 @@ def lichess_batches(F, seed: int, count: int, c960: float = 0.05, variants: floa
     return bodies
 
 
-def main_backend(args):
+def backend_roofline(sizes) -> dict | None:
+    """The actor's device work at each batch count from the committed profile
+    of this tree (profiles/counters.json, workloads "backend:<k>",
+    tools/profile_round.sh): the kernel with the most device time per call
+    (its chess instance when the nets share a kernel), its average duration in
+    the kernel trace and its binding resource.  The actor has no live kernel
+    events, so these times are the profiled run's."""
+    cpath = os.path.join(ROOT, "profiles", "counters.json")
+    if not os.path.exists(cpath):
+        return None
+    db = json.load(open(cpath))
+    tree_ok = db.get("tree") == tree_hash()
+    per = {}
+    for k in sizes:
+        ks = db.get("workloads", {}).get(f"backend:{k}")
+        if not ks:
+            continue
+        focus = {n: r for n, r in ks.items() if r.get("fractions") and r.get("avg_ns")}
+        if not focus:
+            continue
+        total = {n: r["avg_ns"] * (r.get("calls") or 1) for n, r in focus.items()}
+        dom = max(total, key=total.get)
+        r = focus[dom]
+        fr = r["fractions"]
+        per[str(k)] = {"kernel": dom, "instance": r.get("instance"), "avg_ms": round(r["avg_ns"] / 1e6, 4),
+                       "bound": r.get("bound"), "frac": round(fr[r["bound"]], 4),
+                       "fractions": {n: round(v, 4) for n, v in fr.items()},
+                       "waves_per_cu": round(r.get("wave_states", {}).get("mean_waves_per_cu", 0), 2),
+                       "others": {n: {"avg_ms": round(x["avg_ns"] / 1e6, 4), "bound": x.get("bound"),
+                                      "frac": round(x["fractions"][x["bound"]], 4)}
+                                  for n, x in focus.items() if n != dom}}
+    if not per:
+        return None
+    top = per[max(per, key=int)]
+    return {"bound": top["bound"], "frac": top["frac"], "kernel": top["kernel"], "per_batches": per,
+            "counters": {"source": db.get("source"), "tree_matches": tree_ok},
+            "note": "binding resource (largest of VALU-issue / LDS-busy / bytes-past-L2 fractions) of the kernel with "
+                    "the most device time per call, counters per dispatch over its kernel-trace duration in the "
+                    "profiled run of this tree (profiles/counters.json backend:<k>)"}
+
+
+def backend_line(args) -> dict:
     """The drop-in as fishnet would call it: fnnue_backend_go over acquired
     analysis batches (host text in, PositionResponses out, one call = one
     step), at several batch counts per call; the CPU baseline expands and
@@ -322,26 +365,23 @@ def main_backend(args):
     rc = np.zeros(len(bodies), dtype=np.int32)
     t_gen = time.time() - t0
     h = actor._h
+    # the compact form of the answer (fnnue_backend_go_compact): 16 B per position + 24 B per batch
+    cout = (B._Compact * cap)()
+    bout = (B._BatchCompact * len(bodies))()
+    off_c = np.zeros(len(bodies) + 1, dtype=np.uint32)
+    rc_c = np.zeros(len(bodies), dtype=np.int32)
 
     def go(k):
         N.check(N.lib.fnnue_backend_go(h, arr, k, out, cap, N.ptr(off), N.ptr(rc)))
 
-    rows = []
-    for k in sizes:
-        npk = int(plies[:k].sum())
-        for _ in range(max(args.warmup, 1)):
-            go(k)
-        # reps from one probe call: about --go-seconds of wall per batch count
-        tp = time.perf_counter()
-        go(k)
-        probe = time.perf_counter() - tp
-        reps = int(min(2000, max(args.steps if args.steps < 1000 else 3, args.go_seconds / max(probe, 1e-6))))
-        if args.go_calls:
-            reps = args.go_calls
+    def go_compact(k):
+        N.check(N.lib.fnnue_backend_go_compact(h, arr, k, cout, cap, bout, N.ptr(off_c), N.ptr(rc_c), 0))
+
+    def timed(fn, k, reps):
         times, phases = [], []
         for _ in range(reps):
             tp = time.perf_counter()
-            go(k)
+            fn(k)
             times.append(time.perf_counter() - tp)
             phases.append(B.last_stats(actor))
         t = np.array(times)
@@ -349,14 +389,41 @@ def main_backend(args):
               for key in ("prep_ms", "device_ms", "fill_ms", "total_ms")}
         ph["stream_syncs_per_go"] = float(np.mean([p["stream_syncs"] for p in phases]))
         ph["host_threads"] = phases[-1]["host_threads"]
-        assert not rc[:k].any(), "a synthetic batch failed"
+        ph["host_share"] = round((ph["prep_ms"] + ph["fill_ms"]) / max(ph["total_ms"], 1e-9), 3)
+        return t, ph
+
+    rows = []
+    for k in sizes:
+        npk = int(plies[:k].sum())
+        for _ in range(max(args.warmup, 1)):
+            go(k)
+            go_compact(k)
+        # reps from one probe call: about --go-seconds of wall per batch count and form
+        tp = time.perf_counter()
+        go(k)
+        probe = time.perf_counter() - tp
+        reps = int(min(2000, max(args.steps if args.steps < 1000 else 3, args.go_seconds / max(probe, 1e-6))))
+        if args.go_calls:
+            reps = args.go_calls
+        t, ph = timed(go, k, reps)
+        tc, phc = timed(go_compact, k, reps)
+        assert not rc[:k].any() and not rc_c[:k].any(), "a synthetic batch failed"
         rows.append({"batches_per_go": k, "positions_per_go": npk, "calls": reps,
                      "ms_per_go_mean": round(float(t.mean()) * 1e3, 4),
                      "ms_per_go_median": round(float(np.median(t)) * 1e3, 4),
                      "ms_per_go_min": round(float(t.min()) * 1e3, 4),
-                     "positions_per_s": npk / float(t.mean()), "actor_phases_ms": ph})
+                     "positions_per_s": npk / float(t.mean()), "actor_phases_ms": ph,
+                     "compact": {"ms_per_go_mean": round(float(tc.mean()) * 1e3, 4),
+                                 "ms_per_go_median": round(float(np.median(tc)) * 1e3, 4),
+                                 "ms_per_go_min": round(float(tc.min()) * 1e3, 4),
+                                 "positions_per_s": npk / float(tc.mean()), "actor_phases_ms": phc}})
     top = rows[-1]
     kmax = top["batches_per_go"]
+    # the compact answer of the largest call carries the same results as the full records
+    nres = int(off[kmax])
+    compact_same = bool(np.array_equal(off[:kmax + 1], off_c[:kmax + 1]) and all(
+        (cout[i].psqt, cout[i].positional) == (out[i].psqt, out[i].positional) for i in range(0, nres, 97)) and all(
+        cout[i].score == out[i].score for i in range(0, nres, 97)))
     # results of the last (largest) call: parity spot check + CPU baseline on the chess batches
     got_ps = np.array([out[i].psqt for i in range(int(off[kmax]))], dtype=np.int32)
     got_po = np.array([out[i].positional for i in range(int(off[kmax]))], dtype=np.int32)
@@ -402,18 +469,17 @@ def main_backend(args):
                                f"variants HD 512)",
                    "batches_per_go": kmax, "positions_per_go": top["positions_per_go"], "parallelism": "dp1"},
         "backend": rows,
-        "roofline": None,
+        "compact_same_results": compact_same,
+        "roofline": backend_roofline(sizes),
         "cpu_baseline": cpu, "parity_spot_check": parity,
         "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
     }
     del keep
-    print(json.dumps(line), flush=True)
+    return line
 
 
-def main():
-    args = parse_args()
-    if args.workload == "backend":
-        return main_backend(args)
+def run(args) -> dict | None:
+    """One workload (args.workload) measured; rank 0 returns the JSON line."""
     if args.games is None:
         args.games = 5_000 if args.workload == "children" else 10_000
     import torch
@@ -659,6 +725,40 @@ def main():
             small_t = (small_t[0], sp * small_t[0] / max(spl, 1), small_t[2], ss * small_t[0] / max(spl, 1))
     for ctxs in evs:
         ctxs[0].set_timing(False)
+    # Two nets: each net's phases measured ALONE on the stream (one context per
+    # pass, events around every phase).  With both contexts' calls on one
+    # stream, the events of the second context's first phase are stamped
+    # before the first context's last kernel ends (per-net phase
+    # sums past the step), and the dual call overlaps the two nets; so the
+    # per-net costs come from these passes, the two-net step from the timed
+    # steps above.
+    nets_alone = None
+    if len(evs) > 1 and launch == "single":
+        nets_alone = []
+        m = max(5, min(args.steps, 50))
+        for k in range(len(evs)):
+            e = evs[k][0]
+            e.set_timing(True)
+            sync_all()
+            ta = time.perf_counter()
+            for _ in range(m):
+                run_net(k)
+            sync_all()
+            wall = (time.perf_counter() - ta) * 1e3 / m
+            _, pa, fa, sa = e.timing_phases()
+            e.set_timing(False)
+            nets_alone.append({"hd": args.hd if k == 0 else args.small_net, "step_ms": round(wall, 4),
+                               "plan_ms": round(pa / m, 4), "ft_kernel_ms": round(fa / m, 4),
+                               "stack_kernel_ms": round(sa / m, 4),
+                               "phase_sum_ms": round((pa + fa + sa) / m, 4)})
+        if not dual:
+            # the per-net kernel times of this line: each net alone (a launch per step per net here)
+            a0, a1 = nets_alone
+            launches = max(launches, 1)
+            plan_ms, ft_ms, stack_ms = (a0["plan_ms"] * launches, a0["ft_kernel_ms"] * launches,
+                                        a0["stack_kernel_ms"] * launches)
+            l1 = max(small_t[0], 1)
+            small_t = (l1, a1["plan_ms"] * l1, a1["ft_kernel_ms"] * l1, a1["stack_kernel_ms"] * l1)
     check_all()
     if dist_on:
         elapsed_max = D.max_over_ranks(elapsed, torch.device("cuda", local))
@@ -874,7 +974,9 @@ def main():
         "counters": {"source": src, "tree_matches": tree_ok},
         "live_times": ("overlapped: the big and the small net's kernels share the CUs on two streams (dual call); "
                        "counters were profiled per net alone, so these fractions are lower bounds of each kernel's "
-                       "own rate (a --no-dual run gives unshared times)") if dual else "kernel alone on the device",
+                       "own rate (nets_alone: each net's phases alone)") if dual else (
+            "the big net alone on the stream (its own pass; the timed steps run both nets)" if nets_alone
+            else "kernel alone on the device"),
         "note": "frac = the largest of VALU-issue / LDS-busy / HBM fractions of the dominant kernel (counters per "
                 "launch from the committed profile of this tree, over the live kernel time here; peaks at the "
                 "2.4 GHz spec clock); gather_equivalent_GBps = SURVEY §8d algorithmic bytes (every feature row "
@@ -893,7 +995,7 @@ def main():
                                  "counters": {"source": db.get("source"), "tree_matches": tree_ok,
                                               "key": f"{args.workload}@{args.small_net}"},
                                  "live_times": "overlapped with the big net's kernels (dual call)" if dual
-                                 else "second call, alone on the device"}
+                                 else "the small net alone on the stream (its own pass)"}
         small["how"] = ("one fnnue_eval_groups_dual_device call per step: one plan, the small net's FT + stacks on "
                         "the small context's stream beside the big net's FT and stacks" if dual else
                         "a second evaluation call per step on the small net's context")
@@ -932,9 +1034,10 @@ def main():
             "small_net": small,
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
         }
+        if nets_alone is not None:
+            out["nets_alone"] = nets_alone
         if step_ms is not None:
             out["step_ms"] = step_ms
-        print(json.dumps(out), flush=True)
     for ctxs in evs:
         for e in ctxs:
             e.close()
@@ -943,6 +1046,59 @@ def main():
             m.close()
     if dist_on:
         dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
+def extra_lines(args) -> dict:
+    """The default run's extra workloads, measured after
+    the headline and outside its timed steps: BASELINE config 3 with the big +
+    small net through the dual call (20 steps), and the engine actor at 1 / 64
+    / 1024 acquired batches per go(); each with its own oracle spot check."""
+    extra = {}
+    t0 = time.time()
+    a3 = argparse.Namespace(**vars(args))
+    a3.workload, a3.games, a3.small_net, a3.no_dual = "games", 10_000, 128, False
+    a3.steps, a3.warmup, a3.cpu_seconds, a3.no_host_api = 20, 3, 1.0, True
+    o = run(a3)
+    r = o["roofline"]
+    extra["config3_big_small"] = {
+        "workload": o["config"]["workload"], "value": o["value"], "unit": o["unit"], "steps": o["steps"],
+        "ms_per_step": o["ms_per_step"], "dual_call": True,
+        "roofline": {k: r.get(k) for k in ("kernel", "bound", "frac", "kernel_avg_ms", "plan_avg_ms",
+                                           "stack_kernel_avg_ms", "live_times")},
+        "small_net": {k: o["small_net"].get(k) for k in ("hd", "ft_kernel_avg_ms", "stack_kernel_avg_ms",
+                                                         "parity_spot_check")},
+        "nets_alone": o.get("nets_alone"), "parity_spot_check": o["parity_spot_check"],
+        "cpu_baseline": {k: o["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind")}
+        if o.get("cpu_baseline") else None}
+    ab = argparse.Namespace(**vars(args))
+    ab.workload, ab.go_batches, ab.go_seconds, ab.go_calls = "backend", "1,64,1024", 0.3, 0
+    ab.steps, ab.warmup, ab.cpu_seconds = 1000, 3, 1.0
+    o = backend_line(ab)
+    extra["actor"] = {"workload": o["config"]["workload"], "per_batches": [
+        {k: row[k] for k in ("batches_per_go", "positions_per_go", "calls", "ms_per_go_median", "ms_per_go_mean",
+                             "positions_per_s", "actor_phases_ms", "compact")} for row in o["backend"]],
+        "parity_spot_check": o["parity_spot_check"], "compact_same_results": o["compact_same_results"],
+        "roofline": o.get("roofline"),
+        "cpu_baseline": {k: o["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind")}
+        if o.get("cpu_baseline") else None}
+    extra["seconds"] = round(time.time() - t0, 1)
+    return extra
+
+
+def main():
+    args = parse_args()
+    if args.workload == "backend":
+        print(json.dumps(backend_line(args)), flush=True)
+        return
+    default_run = (args.workload == "positions" and args.gpus == 1 and not args.small_net and args.hd == 1024
+                   and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.launch == "auto")
+    out = run(args)
+    if out is None:
+        return
+    if default_run and not args.no_extra:
+        out["extra"] = extra_lines(args)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -139,6 +139,7 @@ SIGNATURES = {
     "fnnue_backend_batch_size": ([_vp, _P(_sz)], _i32),
     "fnnue_backend_go": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp], _i32),
     "fnnue_backend_go_timeout": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp, _u32], _i32),
+    "fnnue_backend_go_compact": ([_vp, _vp, _sz, _vp, _sz, _vp, _vp, _vp, _u32], _i32),
     "fnnue_backend_analysis_json": ([_vp, _sz, C.c_char_p, _sz, _P(_sz)], _i32),
     "fnnue_backend_last_stats": ([_vp, _vp], _i32),
 }

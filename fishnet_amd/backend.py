@@ -43,6 +43,18 @@ class _Response(C.Structure):
                 ("best_move", C.c_char * 8)]
 
 
+class _Compact(C.Structure):
+    _fields_ = [("psqt", C.c_int32), ("positional", C.c_int32), ("score", C.c_int32), ("score_kind", C.c_uint8),
+                ("depth", C.c_uint8), ("flags", C.c_uint8), ("reserved", C.c_uint8)]
+
+
+class _BatchCompact(C.Structure):
+    _fields_ = [("time_ms", C.c_uint64), ("nps", C.c_uint32), ("nodes", C.c_uint32), ("best_move", C.c_char * 8)]
+
+
+COMPACT_SKIPPED, COMPACT_MATRIX, COMPACT_NO_MOVES = 1, 2, 4
+
+
 @dataclass
 class AcquireResponseBody:
     """One acquired batch: work type + id, root FEN, variant, UCI moves, skipPositions."""
@@ -168,6 +180,49 @@ class GpuEvalStub:
                     r.position_id, Score("mate" if r.score_kind == SCORE_MATE else "cp", int(r.score)), r.psqt,
                     r.positional, r.depth, r.nodes, r.time_ms, r.nps, r.best_move.decode() or None,
                     matrix=bool(r.matrix)))
+            res.append(rows)
+        return res
+
+    def go_compact(self, bodies: Sequence[AcquireResponseBody],
+                   timeout_ms: int = 0) -> list[list[PositionResponse] | PositionFailed]:
+        """go() through the compact form (fnnue_backend_go_compact: 16 B per
+        position + 24 B per batch), expanded here into the same
+        PositionResponses the full form gives."""
+        nb = len(bodies)
+        if nb == 0:
+            return []
+        a, _keep = _acquired(bodies)
+        cap = sum(1 if b.work == "move" else len((b.moves if isinstance(b.moves, str) else " ".join(b.moves)).split()) + 1
+                  for b in bodies)
+        out = (_Compact * max(1, cap))()
+        bout = (_BatchCompact * nb)()
+        off = np.zeros(nb + 1, dtype=np.uint32)
+        rc = np.zeros(nb, dtype=np.int32)
+        self.last_batch_rc = rc
+        t0 = time.perf_counter()
+        ret = N.lib.fnnue_backend_go_compact(self._actor._h, a, nb, out, cap, bout, N.ptr(off), N.ptr(rc),
+                                             int(timeout_ms))
+        self.last_call_s = time.perf_counter() - t0
+        N.check(ret)
+        res: list[list[PositionResponse] | PositionFailed] = []
+        for i, b in enumerate(bodies):
+            if rc[i]:
+                res.append(PositionFailed(b.batch_id, int(rc[i])))
+                continue
+            bt = bout[i]
+            rows = []
+            for k in range(int(off[i]), int(off[i + 1])):
+                r = out[k]
+                pid = k - int(off[i])
+                if r.flags & COMPACT_SKIPPED:
+                    rows.append(PositionResponse(pid, None, skipped=True))
+                    continue
+                move = b.work == "move"
+                nodes = 0 if r.flags & COMPACT_NO_MOVES else (bt.nodes if move else 1)
+                rows.append(PositionResponse(
+                    pid, Score("mate" if r.score_kind == SCORE_MATE else "cp", int(r.score)), r.psqt, r.positional,
+                    r.depth, nodes, bt.time_ms, bt.nps, (bt.best_move.decode() or None) if move else None,
+                    matrix=bool(r.flags & COMPACT_MATRIX)))
             res.append(rows)
         return res
 

@@ -33,6 +33,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -69,7 +70,9 @@ double ms_since(Clock::time_point t) { return std::chrono::duration<double, std:
 struct Job {
   const fnnue_acquired* batches = nullptr;
   size_t nb = 0;
-  fnnue_position_response* out = nullptr;
+  fnnue_position_response* out = nullptr;    // the full records, or
+  fnnue_position_compact* cout = nullptr;    // the compact form (fnnue_backend_go_compact) with
+  fnnue_batch_compact* bout = nullptr;       // its per-batch part
   size_t cap = 0;
   uint32_t* off = nullptr;
   int32_t* rc = nullptr;
@@ -180,6 +183,41 @@ void terminal_response(fnnue_position_response& r, uint8_t fin) {
 }
 
 size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// A full response written in place as four stores — bytes 0-15 (position id,
+// the four flag bytes, score), 16-31 (psqt, positional, nodes), 32-47 and
+// 48-55 (time, nps, best move: the same for a whole piece of analysis plies)
+// — instead of a memset and a store per field: the fill is bound by the
+// stores into the caller's buffer.
+static_assert(offsetof(fnnue_position_response, skipped) == 4 && offsetof(fnnue_position_response, score) == 8 &&
+                  offsetof(fnnue_position_response, psqt) == 16 && offsetof(fnnue_position_response, nodes) == 24 &&
+                  offsetof(fnnue_position_response, time_ms) == 32 && offsetof(fnnue_position_response, nps) == 40 &&
+                  offsetof(fnnue_position_response, best_move) == 44 && sizeof(fnnue_position_response) == 56,
+              "fnnue_position_response layout");
+static_assert(sizeof(fnnue_position_compact) == 16 && sizeof(fnnue_batch_compact) == 24, "compact layouts");
+struct ResponseTail {  // bytes 32-55 of an analysis response of one piece
+  __m128i t32;
+  uint64_t t48;
+  ResponseTail(uint64_t ms, uint32_t nps) : t32(_mm_set_epi64x((long long)nps, (long long)ms)), t48(0) {}
+};
+inline uint64_t response_head(uint32_t id, uint8_t skipped, uint8_t kind, uint8_t depth, uint8_t matrix) {
+  return id | (uint64_t)skipped << 32 | (uint64_t)kind << 40 | (uint64_t)depth << 48 | (uint64_t)matrix << 56;
+}
+inline void put_response(fnnue_position_response* r, uint64_t head, int64_t score, int32_t psqt, int32_t positional,
+                         uint64_t nodes, const ResponseTail& tail) {
+  char* d = reinterpret_cast<char*>(r);
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(d), _mm_set_epi64x((long long)score, (long long)head));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(d + 16),
+                   _mm_set_epi64x((long long)nodes, (long long)((uint64_t)(uint32_t)psqt | (uint64_t)(uint32_t)positional << 32)));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(d + 32), tail.t32);
+  std::memcpy(d + 48, &tail.t48, 8);
+}
+inline void put_compact(fnnue_position_compact* r, int32_t psqt, int32_t positional, int32_t score, uint8_t kind,
+                        uint8_t depth, uint8_t flags) {
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(r),
+                   _mm_set_epi32((int)((uint32_t)kind | (uint32_t)depth << 8 | (uint32_t)flags << 16), score,
+                                 positional, psqt));
+}
 
 // The net slot of a batch's variant (shakmaty Variant names, [ref]
 // src/api.rs:304; logger.rs:194-201): standard chess (EngineFlavor::Official
@@ -434,6 +472,7 @@ struct fnnue_backend {
   int recover(Job& j, int k, size_t pi);
   void fill(Job& j, int k, const Piece& P);
   void fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint32_t nps);
+  void fill_hostonly(Job& j, const std::vector<size_t>& all_skipped);
 };
 
 int fnnue_backend::timed_out(const char* where) {
@@ -810,52 +849,61 @@ int fnnue_backend::recover(Job& j, int k, size_t pi) {
 // large pieces): analysis plies as Score::Cp, a game's last ply with no legal
 // move as mate 0 / cp 0; then the move work it carries.  time / nps: the wall
 // time of the go() call until these results were on the host, and the
-// positions evaluated by then per second.
+// positions evaluated by then per second.  Full records or the compact form.
 void fnnue_backend::fill(Job& j, int k, const Piece& P) {
   const auto tf = Clock::now();
   NetWork& W = net[k];
   mark("fill", k, (long)(&P - W.pieces.data()));
-  const char* res = W.down.at<char>(P.down0) - P.o_res;  // the results image, at the piece's offsets
-  const uint8_t* fin = reinterpret_cast<const uint8_t*>(res + P.o_fin);
-  const int32_t* ps = reinterpret_cast<const int32_t*>(res + P.o_ps);
-  const int32_t* po = reinterpret_cast<const int32_t*>(res + P.o_po);
+  const char* res = W.down.at<char>(P.down0);  // the results image from o_res on
+  const uint8_t* fin = reinterpret_cast<const uint8_t*>(res + (P.o_fin - P.o_res));
+  const int32_t* ps = reinterpret_cast<const int32_t*>(res + (P.o_ps - P.o_res));
+  const int32_t* po = reinterpret_cast<const int32_t*>(res + (P.o_po - P.o_res));
   const uint32_t* ply = W.up.at<uint32_t>(P.up0 + P.o_ply);
   filled += P.n + P.nk;
   const double el = ms_since(t0);
   const uint64_t ms = (uint64_t)el;
   const uint32_t nps = el > 0 ? (uint32_t)std::min(4.0e9, (double)filled / (el * 1e-3)) : 0;
   const int32_t nrm = norm;
+  const ResponseTail tail(ms, nps);
   pool.run(P.ng, fill_grain, [&](size_t lo, size_t hi) {
     for (size_t g = lo; g < hi; ++g) {
       const size_t i = P.games[g];
       const uint32_t b = j.off[i], len = j.off[i + 1] - b;
       const uint8_t matrix = j.batches[i].multipv > 0 ? 1 : 0;  // Work::matrix_wanted: multipv is Some
       const bool sk = bskip[i];
-      for (uint32_t q = 0; q < len; ++q) {
-        // written in place: a response built on the stack and copied out
-        // stalls each wide load of the copy on the narrow stores before it
-        // (store forwarding: 1.8x the fill's time on the build host's CPU;
-        // on the GPU box's EPYC within the noise, profiles/r05/backend_fill/)
-        fnnue_position_response& r = j.out[b + q];
-        std::memset(&r, 0, sizeof(r));
-        r.position_id = q;
-        r.time_ms = ms;
-        r.nps = nps;
-        if (sk && skip[b + q]) {
-          r.skipped = 1;
-        } else {
-          const size_t x = ply[g] + q;
-          const int32_t a = ps[x], c = po[x];
-          r.matrix = matrix;
-          r.psqt = a;
-          r.positional = c;
-          r.score_kind = FNNUE_SCORE_CP;
-          r.score = to_cp(a, c, nrm);
-          r.nodes = 1;
-          // The last ply is the only one that can have no legal move (nothing
-          // can be played from it): mate 0 / cp 0 instead of an evaluation.
-          if (q + 1 == len && (fin[g] & kFinalNoMoves)) terminal_response(r, fin[g]);
+      const int32_t* gps = ps + ply[g];
+      const int32_t* gpo = po + ply[g];
+      // The last ply is the only one that can have no legal move (nothing can
+      // be played from it): mate 0 / cp 0 instead of an evaluation.
+      const bool ends = fin[g] & kFinalNoMoves;
+      const uint8_t end_kind = (fin[g] & (kFinalCheck | kFinalExtinct)) ? FNNUE_SCORE_MATE : FNNUE_SCORE_CP;
+      if (j.cout) {
+        fnnue_position_compact* r = j.cout + b;
+        const uint8_t fl = matrix ? FNNUE_COMPACT_MATRIX : 0;
+        for (uint32_t q = 0; q < len; ++q) {
+          if (sk && skip[b + q])
+            put_compact(r + q, 0, 0, 0, 0, 0, FNNUE_COMPACT_SKIPPED);
+          else if (q + 1 == len && ends)
+            put_compact(r + q, gps[q], gpo[q], 0, end_kind, 0, fl | FNNUE_COMPACT_NO_MOVES);
+          else
+            put_compact(r + q, gps[q], gpo[q], (int32_t)to_cp(gps[q], gpo[q], nrm), FNNUE_SCORE_CP, 0, fl);
         }
+        fnnue_batch_compact& B = j.bout[i];
+        B.time_ms = ms;
+        B.nps = nps;
+        B.nodes = 0;
+        std::memset(B.best_move, 0, sizeof(B.best_move));
+        continue;
+      }
+      fnnue_position_response* r = j.out + b;
+      for (uint32_t q = 0; q < len; ++q) {
+        if (sk && skip[b + q])
+          put_response(r + q, response_head(q, 1, 0, 0, 0), 0, 0, 0, 0, tail);
+        else if (q + 1 == len && ends)
+          put_response(r + q, response_head(q, 0, end_kind, 0, matrix), 0, gps[q], gpo[q], 0, tail);
+        else
+          put_response(r + q, response_head(q, 0, FNNUE_SCORE_CP, 0, matrix), to_cp(gps[q], gpo[q], nrm), gps[q],
+                       gpo[q], 1, tail);
       }
     }
   });
@@ -867,15 +915,12 @@ void fnnue_backend::fill(Job& j, int k, const Piece& P) {
 // Move work: a one-ply search over each root's children.
 void fnnue_backend::fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint32_t nps) {
   NetWork& W = net[k];
-  const char* res = W.down.at<char>(P.down0) - P.o_res;
-  const int32_t* kps = reinterpret_cast<const int32_t*>(res + P.o_ps) + P.n;
-  const int32_t* kpo = reinterpret_cast<const int32_t*>(res + P.o_po) + P.n;
+  const char* res = W.down.at<char>(P.down0);
+  const int32_t* kps = reinterpret_cast<const int32_t*>(res + (P.o_ps - P.o_res)) + P.n;
+  const int32_t* kpo = reinterpret_cast<const int32_t*>(res + (P.o_po - P.o_res)) + P.n;
   for (size_t t = 0; t < W.roots.size(); ++t) {
     const MoveRoot& R = W.mroots[t];
-    fnnue_position_response& r = j.out[j.off[W.roots[t]]];
-    std::memset(&r, 0, sizeof(r));
-    r.time_ms = ms;
-    r.nps = nps;
+    const size_t i = W.roots[t];
     // rank: 2 = mates, 1 = evaluated, 0 = never (value orders within a rank)
     size_t best = 0;
     int best_rank = -1;
@@ -900,18 +945,77 @@ void fnnue_backend::fill_roots(Job& j, int k, const Piece& P, uint64_t ms, uint3
       }
     }
     const size_t x = W.kid_first[t] + best;
+    const uint8_t kind = best_rank == 2 ? FNNUE_SCORE_MATE : FNNUE_SCORE_CP;
+    const int64_t score = best_rank == 2 ? 1 : bv * 100 / norm;
+    if (j.cout) {
+      put_compact(j.cout + j.off[i], -kps[x], -kpo[x], (int32_t)score, kind, 1, 0);
+      fnnue_batch_compact& B = j.bout[i];
+      B.time_ms = ms;
+      B.nps = nps;
+      B.nodes = (uint32_t)R.uci.size();
+      std::memset(B.best_move, 0, sizeof(B.best_move));
+      std::strncpy(B.best_move, R.uci[best].c_str(), sizeof(B.best_move) - 1);
+      continue;
+    }
+    fnnue_position_response& r = j.out[j.off[i]];
+    std::memset(&r, 0, sizeof(r));
+    r.time_ms = ms;
+    r.nps = nps;
     r.psqt = -kps[x];
     r.positional = -kpo[x];
     r.depth = 1;
     r.nodes = R.uci.size();
-    if (best_rank == 2) {
-      r.score_kind = FNNUE_SCORE_MATE;
-      r.score = 1;
-    } else {
-      r.score_kind = FNNUE_SCORE_CP;
-      r.score = bv * 100 / norm;
-    }
+    r.score_kind = kind;
+    r.score = score;
     std::strncpy(r.best_move, R.uci[best].c_str(), sizeof(r.best_move) - 1);
+  }
+}
+
+// The batches answered without the device: move-work roots without a legal
+// move, analysis batches whose every position is skipped.
+void fnnue_backend::fill_hostonly(Job& j, const std::vector<size_t>& all_skipped) {
+  const double el = ms_since(t0);
+  const uint64_t ms = (uint64_t)el;
+  const uint32_t nps = el > 0 ? (uint32_t)std::min(4.0e9, (double)filled / (el * 1e-3)) : 0;
+  auto batch = [&](size_t i) {
+    fnnue_batch_compact& B = j.bout[i];
+    std::memset(&B, 0, sizeof(B));
+    B.time_ms = ms;
+    B.nps = nps;
+  };
+  for (int k = 0; k < kKinds; ++k) {
+    NetWork& W = net[k];
+    for (size_t t = 0; t < W.terminal.size(); ++t) {
+      const size_t i = W.terminal[t];
+      const uint8_t fin = W.troots[t].fin;
+      if (j.cout) {
+        put_compact(j.cout + j.off[i], 0, 0, 0,
+                    (fin & (kFinalCheck | kFinalExtinct)) ? FNNUE_SCORE_MATE : FNNUE_SCORE_CP, 0,
+                    FNNUE_COMPACT_NO_MOVES);
+        batch(i);
+        continue;
+      }
+      fnnue_position_response& r = j.out[j.off[i]];
+      std::memset(&r, 0, sizeof(r));
+      r.time_ms = ms;
+      r.nps = nps;
+      terminal_response(r, fin);
+    }
+  }
+  for (size_t i : all_skipped) {
+    if (j.cout) batch(i);
+    for (uint32_t q = j.off[i]; q < j.off[i + 1]; ++q) {
+      if (j.cout) {
+        put_compact(j.cout + q, 0, 0, 0, 0, 0, FNNUE_COMPACT_SKIPPED);
+        continue;
+      }
+      fnnue_position_response& r = j.out[q];
+      std::memset(&r, 0, sizeof(r));
+      r.position_id = q - j.off[i];
+      r.skipped = 1;
+      r.time_ms = ms;
+      r.nps = nps;
+    }
   }
 }
 
@@ -1104,30 +1208,9 @@ void fnnue_backend::run(Job& j) {
     j.err = g_err;
     return;
   }
-  const double el = ms_since(t0);
-  const uint64_t ms = (uint64_t)el;
-  const uint32_t nps = el > 0 ? (uint32_t)std::min(4.0e9, (double)filled / (el * 1e-3)) : 0;
+  fill_hostonly(j, all_skipped);
   uint32_t npieces = 0;
-  for (int k = 0; k < kKinds; ++k) {
-    NetWork& W = net[k];
-    npieces += (uint32_t)W.pieces.size();
-    for (size_t t = 0; t < W.terminal.size(); ++t) {
-      fnnue_position_response& r = j.out[j.off[W.terminal[t]]];
-      std::memset(&r, 0, sizeof(r));
-      r.time_ms = ms;
-      r.nps = nps;
-      terminal_response(r, W.troots[t].fin);
-    }
-  }
-  for (size_t i : all_skipped)
-    for (uint32_t q = j.off[i]; q < j.off[i + 1]; ++q) {
-      fnnue_position_response& r = j.out[q];
-      std::memset(&r, 0, sizeof(r));
-      r.position_id = q - j.off[i];
-      r.skipped = 1;
-      r.time_ms = ms;
-      r.nps = nps;
-    }
+  for (const NetWork& W : net) npieces += (uint32_t)W.pieces.size();
   j.ret = FNNUE_OK;
   mark("done");
   if (trace) std::fprintf(stderr, "FNNUE_BACKEND_TRACE {\"batches\":%zu,\"marks\":[%s]}\n", nb, tl.c_str());
@@ -1277,15 +1360,11 @@ void fnnue_backend_free(fnnue_backend* b) {
   reap_abandoned();
 }
 
-int fnnue_backend_go_timeout(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches,
-                             fnnue_position_response* out, size_t cap, uint32_t* off, int32_t* batch_rc,
-                             uint32_t timeout_ms) {
-  if (!b || !off || !batch_rc || (nbatches && !batches) || (cap && !out)) return fail(FNNUE_E_ARG, "null argument");
-  if (nbatches > (1u << 24)) return fail(FNNUE_E_ARG, "too many batches");
-  Job j;
+namespace {
+int go_job(fnnue_backend* b, Job& j, const fnnue_acquired* batches, size_t nbatches, size_t cap, uint32_t* off,
+           int32_t* batch_rc, uint32_t timeout_ms) {
   j.batches = batches;
   j.nb = nbatches;
-  j.out = out;
   j.cap = cap;
   j.off = off;
   j.rc = batch_rc;
@@ -1301,6 +1380,30 @@ int fnnue_backend_go_timeout(fnnue_backend* b, const fnnue_acquired* batches, si
   b->run(j);
   if (j.ret) return fail(j.ret, j.err);
   return FNNUE_OK;
+}
+}  // namespace
+
+int fnnue_backend_go_timeout(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches,
+                             fnnue_position_response* out, size_t cap, uint32_t* off, int32_t* batch_rc,
+                             uint32_t timeout_ms) {
+  if (!b || !off || !batch_rc || (nbatches && !batches) || (cap && !out)) return fail(FNNUE_E_ARG, "null argument");
+  if (nbatches > (1u << 24)) return fail(FNNUE_E_ARG, "too many batches");
+  Job j;
+  j.out = out;
+  return go_job(b, j, batches, nbatches, cap, off, batch_rc, timeout_ms);
+}
+
+int fnnue_backend_go_compact(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches,
+                             fnnue_position_compact* out, size_t cap, fnnue_batch_compact* bout, uint32_t* off,
+                             int32_t* batch_rc, uint32_t timeout_ms) {
+  if (!b || !off || !batch_rc || (nbatches && (!batches || !bout)) || (cap && !out))
+    return fail(FNNUE_E_ARG, "null argument");
+  if (nbatches > (1u << 24)) return fail(FNNUE_E_ARG, "too many batches");
+  if (b->norm < 13) return fail(FNNUE_E_ARG, "compact results need normalize_to_pawn >= 13 (32-bit scores)");
+  Job j;
+  j.cout = out;
+  j.bout = bout;
+  return go_job(b, j, batches, nbatches, cap, off, batch_rc, timeout_ms);
 }
 
 int fnnue_backend_go(fnnue_backend* b, const fnnue_acquired* batches, size_t nbatches, fnnue_position_response* out,

@@ -376,7 +376,7 @@ hipEvent_t mid_event(std::array<hipEvent_t, 4>* ev) { return ev ? (*ev)[1] : nul
 extern "C" {
 
 const char* fnnue_last_error(void) { return g_err.c_str(); }
-uint32_t fnnue_abi_version(void) { return (3u << 16) | 0u; }
+uint32_t fnnue_abi_version(void) { return (3u << 16) | 1u; }  // 3.1: fnnue_backend_go_timeout, FNNUE_E_TIMEOUT
 
 int fnnue_net_load_mem(const void* buf, size_t len, fnnue_net** out) {
   if (!buf || !out) return fail(FNNUE_E_ARG, "null argument");

@@ -156,6 +156,47 @@ int fnnue_backend_go_timeout(fnnue_backend *b, const fnnue_acquired *batches, si
                              fnnue_position_response *out, size_t cap, uint32_t *off, int32_t *batch_rc,
                              uint32_t timeout_ms);
 
+/* The compact form of a go()'s answer (16 B per position instead of 56, and
+ * what is the same for all of a batch's positions once per batch): what a
+ * caller that builds its own response objects needs — fishnet's actor builds
+ * PositionResponse (ipc.rs:28-39) in Rust memory anyway, so the 56-byte C
+ * record is an intermediate it need not pay for.  Same semantics as
+ * fnnue_position_response field by field:
+ *   nodes     = 0 when flags has FNNUE_COMPACT_SKIPPED or FNNUE_COMPACT_NO_MOVES,
+ *               else 1 for an analysis position, fnnue_batch_compact.nodes for
+ *               the answer of a move batch;
+ *   best_move = fnnue_batch_compact.best_move (move work), else none;
+ *   time_ms / nps = the batch's (every position of a batch gets its piece's).
+ * score is 32-bit: exact for normalize_to_pawn >= 13 (|psqt + positional| <
+ * 2^32), which the compact call requires. */
+#define FNNUE_COMPACT_SKIPPED 1   /* Skip::Skip: nothing else set */
+#define FNNUE_COMPACT_MATRIX 2    /* serialise as AnalysisPart::Matrix */
+#define FNNUE_COMPACT_NO_MOVES 4  /* a position without a legal move: mate 0 / cp 0, nodes 0, depth 0 */
+typedef struct {
+  int32_t psqt;
+  int32_t positional;
+  int32_t score;         /* centipawns or mate (score_kind), side to move */
+  uint8_t score_kind;    /* FNNUE_SCORE_* */
+  uint8_t depth;
+  uint8_t flags;         /* FNNUE_COMPACT_* */
+  uint8_t reserved;
+} fnnue_position_compact;
+
+typedef struct {
+  uint64_t time_ms;      /* wall time of the go() call until the batch's piece was back on the host */
+  uint32_t nps;          /* positions evaluated by then, per second */
+  uint32_t nodes;        /* move work: the legal children searched (0 for a root without one); analysis: 0 */
+  char best_move[8];     /* move work: UCI, NUL-terminated; "" otherwise */
+} fnnue_batch_compact;
+
+/* go() answering in the compact form: batch i's positions in out[off[i] ..
+ * off[i + 1]) (cap = capacity of out), its per-batch part in bout[i]; budget
+ * and errors as fnnue_backend_go_timeout.  FNNUE_E_ARG when the channel's
+ * normalize_to_pawn is below 13. */
+int fnnue_backend_go_compact(fnnue_backend *b, const fnnue_acquired *batches, size_t nbatches,
+                             fnnue_position_compact *out, size_t cap, fnnue_batch_compact *bout, uint32_t *off,
+                             int32_t *batch_rc, uint32_t timeout_ms);
+
 /* Where the last go() spent its time (diagnostics; the reference's engine
  * reports only time / nps per position).  Each net's games are cut into pieces
  * of about FNNUE_BACKEND_PIECE_PLIES plies (default 524288); a piece is one

@@ -117,3 +117,15 @@ def test_batch_size_counts_tokens_like_the_builder():
             n = C.c_size_t()
             N.check(N.lib.fnnue_backend_batch_size(C.byref(a), C.byref(n)))
             assert n.value == len(text.split()) + 1, (repr(text), shift)
+
+
+def test_compact_layouts_and_argument_checks():
+    """The compact answer's records (fnnue_backend.h) have the C layout the
+    library writes, and the go() forms reject null arguments without a
+    device."""
+    import ctypes as C
+    assert C.sizeof(B._Compact) == 16 and C.sizeof(B._BatchCompact) == 24
+    assert C.sizeof(B._Response) == 56 and C.sizeof(B._Init) == 8
+    assert N.lib.fnnue_backend_go_compact(None, None, 0, None, 0, None, None, None, 0) == -1
+    assert N.lib.fnnue_backend_go_timeout(None, None, 0, None, 0, None, None, 5) == -1
+    assert N.ERRORS[-11] == "FNNUE_E_TIMEOUT"

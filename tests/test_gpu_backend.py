@@ -571,3 +571,40 @@ def test_go_timeout_breaks_the_channel():
             check_rows(on, bodies[i], big[i])
     finally:
         actor2.close()
+
+
+def test_compact_form_equals_full_records(chan):
+    """fnnue_backend_go_compact (16 B per position + 24 B per batch) carries
+    exactly what the full PositionResponse records do, for every kind of
+    batch: analysis (chess, Chess960, crazyhouse, atomic), games ending in
+    mate / stalemate / explosion, skipPositions and all-skipped batches,
+    MultiPV, move work (best child, mate in one, mated and stalemated roots),
+    and failing batches with the same codes."""
+    stub, on = chan
+    bodies = [B.AcquireResponseBody(str(g["id"]), g["position"], g["moves"]) for g in GAMES[:30]]
+    bodies += [B.AcquireResponseBody("c960", C960, F.random_game(7, C960, 60), variant="chess960"),
+               B.AcquireResponseBody("mate", START, FOOLS_MATE),
+               B.AcquireResponseBody("stalemate", STALEMATE[0], STALEMATE[1], variant="fromPosition"),
+               B.AcquireResponseBody("boom", START, ATOMIC_WIN, variant="atomic"),
+               B.AcquireResponseBody("zh", ZH_START, F.random_vgame(3, ZH, ZH_START, 70), variant="crazyhouse"),
+               B.AcquireResponseBody("skip", GAMES[3]["position"], GAMES[3]["moves"], skip_positions=[0, 2, 5]),
+               B.AcquireResponseBody("allskip", START, "e2e4", skip_positions=[0, 1]),
+               B.AcquireResponseBody("mpv", START, "e2e4 e7e5", multipv=2),
+               B.AcquireResponseBody("mv", GAMES[1]["position"], " ".join(GAMES[1]["moves"].split()[:30]), work="move"),
+               B.AcquireResponseBody("m1", START, "f2f3 e7e5 g2g4", work="move"),
+               B.AcquireResponseBody("mated", START, FOOLS_MATE, work="move"),
+               B.AcquireResponseBody("stale", STALEMATE[0], STALEMATE[1], work="move"),
+               B.AcquireResponseBody("zhmv", ZH_START, "e2e4 d7d5 e4d5 d8d5", work="move", variant="crazyhouse"),
+               B.AcquireResponseBody("badmove", START, "e2e4 e7e5 e1e3"),
+               B.AcquireResponseBody("anti", START, "e2e4", variant="antichess")]
+    full = stub.go(bodies)
+    comp = stub.go_compact(bodies)
+    key = lambda r: (r.position_id, r.score, r.psqt, r.positional, r.depth, r.nodes, r.best_move, r.skipped, r.matrix)
+    for b, f, c in zip(bodies, full, comp):
+        if isinstance(f, B.PositionFailed):
+            assert isinstance(c, B.PositionFailed) and c.code == f.code, b.batch_id
+            continue
+        assert [key(r) for r in f] == [key(r) for r in c], b.batch_id
+        assert all(r.time_ms == c[0].time_ms and r.nps == c[0].nps for r in c if not r.skipped)
+    for i in range(30):
+        check_rows(on, bodies[i], comp[i])

@@ -7,6 +7,8 @@
 #include <cstdio>
 #include <cstring>
 #include <vector>
+#include <emmintrin.h>
+#include <cstddef>
 #include "../../include/fnnue_backend.h"
 static inline int64_t to_cp(int32_t psqt, int32_t positional, int32_t norm) {
   const int64_t v = ((int64_t)psqt + positional) / 16;
@@ -22,7 +24,7 @@ int main() {
   std::vector<int32_t> ps(n), po(n);
   for (size_t i = 0; i < n; ++i) { ps[i] = (int)(i * 2654435761u) % 40000 - 20000; po[i] = (int)(i * 40503u) % 30000 - 15000; }
   volatile int32_t nv = 361; int32_t nrm = nv;
-  for (int variant = 0; variant < 5; ++variant) {
+  for (int variant = 0; variant < 6; ++variant) {
     double best = 1e9;
     for (int rep = 0; rep < 50; ++rep) {
       auto t0 = std::chrono::steady_clock::now();
@@ -36,6 +38,22 @@ int main() {
           r.score_kind = 1;
           r.score = to_cp(ps[q], po[q], nrm);
           r.nodes = 1;
+        }
+      } else if (variant == 5) {
+        // three 16-byte stores and one 8-byte store per record; the time / nps
+        // / best-move bytes are the same for the whole piece
+        static_assert(offsetof(fnnue_position_response, score) == 8 && offsetof(fnnue_position_response, psqt) == 16 &&
+                      offsetof(fnnue_position_response, time_ms) == 32 && sizeof(fnnue_position_response) == 56, "");
+        const __m128i hi = _mm_set_epi64x((long long)7, (long long)5);
+        char* base = reinterpret_cast<char*>(out.data());
+        for (size_t q = 0; q < n; ++q) {
+          char* r = base + 56 * q;
+          const int64_t sc = to_cp(ps[q], po[q], nrm);
+          _mm_storeu_si128(reinterpret_cast<__m128i*>(r), _mm_set_epi64x(sc, (long long)(uint32_t)q));
+          _mm_storeu_si128(reinterpret_cast<__m128i*>(r + 16),
+                           _mm_set_epi64x(1, (long long)((uint64_t)(uint32_t)ps[q] | (uint64_t)(uint32_t)po[q] << 32)));
+          _mm_storeu_si128(reinterpret_cast<__m128i*>(r + 32), hi);
+          _mm_storel_epi64(reinterpret_cast<__m128i*>(r + 48), _mm_setzero_si128());
         }
       } else if (variant == 4) {
         for (size_t q = 0; q < n; ++q) {

@@ -8,7 +8,8 @@
 # then tools/roofline.py turns them into gpurun_out/prof_<tag>/counters.json.
 #   usage: tools/profile_round.sh <tag> [workload ...]   (default: all of them)
 # A workload "<name>@<hd>" profiles bench.py --workload <name> --hd <hd>
-# (counters keyed so; bench.py reads them for that width, e.g. the small net).
+# (counters keyed so; bench.py reads them for that width, e.g. the small net);
+# "backend:<k>" profiles the engine actor at <k> batches per go().
 set -uo pipefail
 TAG=${1:-rXX}; shift || true
 WLS=${*:-positions games children crazyhouse atomic crazyhouse-games atomic-games}
@@ -24,10 +25,12 @@ SETS=(
 for wl in $WLS; do
   args="--workload ${wl%@*}"
   [[ $wl == *@* ]] && args="$args --hd ${wl#*@}"
+  # backend:<k>: the engine actor at <k> acquired batches per go() (bench.py --workload backend)
+  [[ $wl == backend:* ]] && args="--workload backend --go-batches ${wl#backend:} --go-calls 20"
   D=$OUT/$wl
   mkdir -p "$D"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api $args > "$D/trace.log" 2>&1
+    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api --no-extra $args > "$D/trace.log" 2>&1
   rc=$?
   echo "[$wl trace] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
@@ -35,7 +38,7 @@ for wl in $WLS; do
   for pmc in "${SETS[@]}"; do
     i=$((i + 1))
     timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d "$D/pmc_$i" -o run -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-api $args > "$D/pmc_$i.log" 2>&1
+      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-api --no-extra $args > "$D/pmc_$i.log" 2>&1
     rc=$?
     echo "[$wl pmc $i: $pmc] rc=$rc"
     [ $rc -eq 0 ] || exit $rc

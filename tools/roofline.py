@@ -40,14 +40,17 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CUS, SIMDS, XCDS, HBM_PEAK, CLOCK = 256, 1024, 8, 8.0e12, 2.4e9
-FOCUS = ("ft_slices_kernel", "ft_segments_kernel", "stack_kernel", "ft_scratch_kernel", "ft_groups_kernel")
+FOCUS = ("ft_slices_kernel", "ft_segments_kernel", "stack_kernel", "ft_scratch_kernel", "ft_groups_kernel",
+         "replay_pair_kernel", "replay_wave_kernel")
 
 
 def tree_hash() -> str:
     """sha256 over the sources of the evaluation kernels (what their counters depend on)."""
     h = hashlib.sha256()
     src = os.path.join(ROOT, "fishnet_amd", "csrc")
-    files = ("kernels.hip", "ft_sliced.hip", "ft_segments.hip", "device_common.h", "sliced_common.h", "kernels.h")
+    files = ("kernels.hip", "ft_sliced.hip", "ft_segments.hip", "device_common.h", "sliced_common.h", "kernels.h",
+             # the engine actor's replay (backend:<k> workloads)
+             "builder.hip", "vbuilder.hip", "replay_wave.h", "board.h", "vboard.h")
     for f in sorted(os.path.join(src, f) for f in files):
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
@@ -64,18 +67,28 @@ def workload(d: str) -> dict:
     stats = os.path.join(d, "trace", "run_kernel_stats.csv")
     for r in csv.DictReader(open(stats)):
         k = kname(r["Name"])
-        if k in dur:  # several template instances: keep the busiest
+        if k in dur:  # several template instances (e.g. the actor's chess and variant nets): keep the busiest
             if float(r["TotalDurationNs"]) <= dur[k]["total_ns"]:
                 continue
-        dur[k] = {"avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"]), "total_ns": float(r["TotalDurationNs"])}
+        dur[k] = {"avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"]), "total_ns": float(r["TotalDurationNs"]),
+                  "full": r["Name"]}
+    # counters per instance; a kernel's are those of the instance its time is (the busiest)
     ctr = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "pmc_*", "run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            ctr[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            ctr[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    by_short = collections.defaultdict(list)
+    for full in ctr:
+        by_short[kname(full)].append(full)
     out = {}
-    for k in sorted(set(dur) | set(ctr)):
-        c = {n: sum(v) / len(v) for n, v in ctr.get(k, {}).items()}
+    for k in sorted(set(dur) | set(by_short)):
+        full = dur.get(k, {}).get("full")
+        if full not in ctr:
+            full = by_short[k][0] if len(by_short.get(k, [])) == 1 else None
+        c = {n: sum(v) / len(v) for n, v in ctr.get(full, {}).items()} if full else {}
         rec = {"avg_ns": dur.get(k, {}).get("avg_ns"), "calls": dur.get(k, {}).get("calls"), "counters": c}
+        if full and len(by_short.get(k, [])) > 1:
+            rec["instance"] = full
         t = rec["avg_ns"]
         if k in FOCUS and t and c:
             cyc = CLOCK * t * 1e-9
