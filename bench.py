@@ -74,6 +74,9 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=1000,
                     help="timed steps (1000: ~1.5 s of config 2, long enough for an SMI sampler to see the GPU busy)")
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle-s", type=float, default=0.3,
+                    help="untimed steps for this many seconds before the warm-up steps (the GPU's clock ramp out of "
+                         "the host-only setup; 0: none)")
     ap.add_argument("--workload", choices=["positions", "games", "children", "crazyhouse", "atomic", "crazyhouse-games",
                                            "atomic-games", "backend"], default="positions")
     ap.add_argument("--go-batches", default="1,64,1024,16384",
@@ -680,6 +683,20 @@ def run(args) -> dict | None:
     if diag_stream is not None:
         torch.cuda.set_stream(diag_stream)
         streams = [diag_stream.cuda_stream]
+    # Clock settle (untimed, before the W warm-up steps): the GPU leaves its
+    # idle clock over ~25 steps of sustained work after the host-only setup
+    # phase (profiles/r05/driver_gap: a 20-step window after 5 warm-up steps
+    # averaged that ramp, 1.58 -> 1.41 ms per step).  The steps are run, in
+    # full, until `settle_s` of wall time has passed; the timed steps then see
+    # the steady state a serving process runs at.  Reported as "settle".
+    settle_steps, ts = 0, time.perf_counter()
+    while args.settle_s > 0 and time.perf_counter() - ts < args.settle_s and settle_steps < 10_000:
+        step()
+        settle_steps += 1
+        if settle_steps % 8 == 0:
+            sync_all()
+    sync_all()
+    settle = {"steps": settle_steps, "s": round(time.perf_counter() - ts, 3)}
     for _ in range(args.warmup):
         step()
     sync_all()
@@ -1033,6 +1050,7 @@ def run(args) -> dict | None:
             "host_api": host_api,
             "small_net": small,
             "setup_s": {"net": round(t_net, 2), "inputs": round(t_gen, 2)},
+            "settle": settle,
         }
         if nets_alone is not None:
             out["nets_alone"] = nets_alone

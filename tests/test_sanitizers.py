@@ -47,3 +47,23 @@ def test_backend_thread_pool_under_tsan(tmp_path):
     r = subprocess.run([str(out)], capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "workers stress ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+@pytest.mark.parametrize("mode", ["asan", "ubsan"])
+def test_move_text_scan_sanitized(tmp_path, mode):
+    """The engine actor's scan of server-supplied move text
+    (fishnet_amd/csrc/text_scan.h): under ASan + UBSan (the scalar
+    form, every read inside the caller's allocation) and under UBSan alone
+    (the 16-byte form against the scalar one, strings at every alignment and
+    ending on a page whose successor is inaccessible)."""
+    out = tmp_path / f"text_scan_{mode}"
+    flags = SAN if mode == "asan" else ["-fsanitize=undefined", "-fno-sanitize-recover=all", "-g", "-O2",
+                                          "-march=x86-64-v3"]
+    subprocess.run(["g++", "-std=c++17", *flags, os.path.join(ROOT, "tests/sanitize/text_scan_check.cpp"),
+                    "-o", str(out)], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([str(out)], capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "text scan ok" in r.stdout
