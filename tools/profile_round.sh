@@ -30,7 +30,7 @@ for wl in $WLS; do
   D=$OUT/$wl
   mkdir -p "$D"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-api --no-extra $args > "$D/trace.log" 2>&1
+    python3 bench.py --steps 10 --warmup 2 --settle-s 0 --no-cpu-baseline --no-host-api --no-extra $args > "$D/trace.log" 2>&1
   rc=$?
   echo "[$wl trace] rc=$rc"
   [ $rc -eq 0 ] || exit $rc
@@ -38,7 +38,7 @@ for wl in $WLS; do
   for pmc in "${SETS[@]}"; do
     i=$((i + 1))
     timeout -s KILL 120 rocprofv3 --pmc $pmc --output-format csv -d "$D/pmc_$i" -o run -- \
-      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-api --no-extra $args > "$D/pmc_$i.log" 2>&1
+      python3 bench.py --steps 3 --warmup 1 --settle-s 0 --no-cpu-baseline --no-host-api --no-extra $args > "$D/pmc_$i.log" 2>&1
     rc=$?
     echo "[$wl pmc $i: $pmc] rc=$rc"
     [ $rc -eq 0 ] || exit $rc
