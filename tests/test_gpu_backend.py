@@ -264,6 +264,50 @@ def test_concurrent_callers(chan):
             check_rows(on, b, rows)
 
 
+def test_two_channels_on_one_device_at_once(chan):
+    """Two channels (fishnet: two workers, each its own engine) on the same
+    device, driven from two threads at once, each call a different mix of
+    chess, Chess960 and variant batches: each channel's answers equal the same
+    batches answered alone on the module's channel, and sampled plies equal the
+    oracle (the channels share no buffers, streams or error words)."""
+    stub, on = chan
+    data = net_bytes(1, 1024, 0)
+    stub2, actor2 = B.channel(F.Net.from_bytes(data), 0,
+                              crazyhouse=F.Net.from_bytes_variant(F.synthesize_variant_net(5, 512, ZH), ZH),
+                              atomic=F.Net.from_bytes_variant(F.synthesize_variant_net(6, 512, AT), AT))
+    try:
+        mk = lambda off: ([B.AcquireResponseBody(f"g{off + i}", GAMES[(off + i) % len(GAMES)]["position"],
+                                                 GAMES[(off + i) % len(GAMES)]["moves"]) for i in range(300)]
+                          + [B.AcquireResponseBody(f"c{off}", C960, F.random_game(off + 3, C960, 80), variant="chess960"),
+                             B.AcquireResponseBody(f"z{off}", ZH_START, F.random_vgame(off + 4, ZH, ZH_START, 90),
+                                                   variant="crazyhouse")])
+        sets = [mk(0), mk(300)]
+        alone = [stub.go(s) for s in sets]
+        out = [[None] * 6 for _ in range(2)]
+
+        def worker(t):
+            st = stub if t == 0 else stub2
+            for r in range(6):
+                out[t][r] = st.go(sets[t])
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        key = lambda r: (r.position_id, r.score, r.psqt, r.positional, r.skipped)
+        for t in range(2):
+            for r in range(6):
+                for b, x, y in zip(sets[t], alone[t], out[t][r]):
+                    assert not isinstance(y, B.PositionFailed), (t, r, b.batch_id)
+                    assert [key(q) for q in x] == [key(q) for q in y], (t, r, b.batch_id)
+            for i in range(0, 300, 37):
+                check_rows(on, sets[t][i], out[t][5][i])
+            check_rows(on, sets[t][301], out[t][5][301], ZH)
+    finally:
+        actor2.close()
+
+
 # Positions where a UCI token's meaning is subtle: castling both ways and in
 # Chess960 (king already on its destination, rook beside it), en passant
 # (legal, and exposing the own king), promotions with and without capture,
