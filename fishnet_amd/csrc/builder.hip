@@ -621,6 +621,138 @@ struct ChessRules {
     b.stm = (uint32_t)(us ^ 1);
     return true;
   }
+  // The whole window's chain lane-parallel (lane j = move j), for the same
+  // boards, moves and ep words as k calls of step().  step() needs the board
+  // only for the mover's piece pc (castling is the own king onto a castling
+  // square, ep and the double push need a pawn); every other effect is a
+  // select on known squares.  So:
+  //   1. the piece on from_j before move j is what the last earlier move that
+  //      wrote from_j put there (an LDS table of writers per square, one
+  //      64-bit mask each: the highest writer below j), or the window's first
+  //      board; a write puts the mover's piece (or its promotion), so the
+  //      pieces follow by pointer jumping over the writers (6 rounds);
+  //   2. castling moves are detected from those pieces; a castling move writes
+  //      two squares (king to kto, rook to rto), so if any, step 1 runs again
+  //      with them;
+  //   3. ep squares by a shuffle from the move before, en passant captures;
+  //   4. the snapshots, square = lane, one select chain per move on values
+  //      that are all known (no per-move readlane of the board).
+  // Exact for every move up to a window's first illegal one (the only part
+  // check() and the records use): with all earlier moves legal, each mover's
+  // square was last written by an earlier move or holds its first-board
+  // piece; a castling move kills its colour's rights (its king's square is
+  // touched), so no later detection depends on step 2's second pass; a move
+  // whose piece the table gets wrong (it moves from a square emptied since)
+  // is illegal on its exact board, and fails its check as in step().
+  static constexpr bool kLaneChain = true;
+  __device__ static uint32_t lane_chain(Scalars& sc, uint32_t& sqv, uint32_t myc, uint32_t k, const Win& w,
+                                        uint32_t (*SNAP)[16], int lane, uint32_t& mvw, uint32_t (&scw)[kVary]) {
+    reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
+    const uint64_t badm = __ballot((uint32_t)lane < k && (myc & replay::kTokBad));
+    const uint32_t kplay = badm ? min(k, (uint32_t)__builtin_ctzll(badm)) : k;
+    const bool live = (uint32_t)lane < kplay;
+    const int from = (int)replay::tok_from(myc), to = (int)replay::tok_to(myc), promo = (int)replay::tok_piece(myc);
+    const int us = (int)(sc.stm ^ ((uint32_t)lane & 1u));
+    const int back = us == WHITE ? 0 : 56;
+    const uint32_t start = (uint32_t)__shfl((int)sqv, from, 64);  // the first board's piece on from
+    // writers table: rows 57-64 of this window's snapshot buffer (written
+    // only by step 4, after their last use here)
+    uint64_t* WR = reinterpret_cast<uint64_t*>(SNAP[57]);
+    int w1 = to, w2 = 64;  // squares a move writes (64: none)
+    // piece on from_j before move j (S) through the writers of step 1
+    auto resolve = [&]() -> uint32_t {
+      WR[lane] = 0;
+      replay::lds_fence();
+      if (live) {
+        atomicOr(reinterpret_cast<unsigned long long*>(&WR[w1]), 1ull << lane);
+        if (w2 < 64) atomicOr(reinterpret_cast<unsigned long long*>(&WR[w2]), 1ull << lane);
+      }
+      replay::lds_fence();
+      const uint64_t m = WR[from] & ((1ull << lane) - 1);
+      replay::lds_fence();  // the table's reads before a second pass clears it
+      const int src = m ? 63 - __builtin_clzll(m) : 0;
+      const int sw1 = __shfl(w1, src, 64), spr = __shfl(promo, src, 64);
+      const int sus = (int)(sc.stm ^ ((uint32_t)src & 1u));
+      bool known = true;
+      uint32_t val = start;
+      if (m) {
+        if (sw1 != from) val = (uint32_t)make_piece_d(sus, ROOK);  // a castling move's rook square
+        else if (spr) val = (uint32_t)make_piece_d(sus, spr);      // a promotion
+        else known = false;                                         // that move's own piece
+      }
+      int link = src;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const uint32_t lv = (uint32_t)__shfl((int)val, link, 64);
+        const int lk = __shfl((int)known, link, 64), ll = __shfl(link, link, 64);
+        if (!known) {
+          if (lk) {
+            val = lv;
+            known = true;
+          } else {
+            link = ll;
+          }
+        }
+      }
+      return val;
+    };
+    uint32_t pc = resolve();
+    // castling: step()'s test with this move's rights
+    auto castle_rook = [&](uint32_t p) -> int {
+      int rsq = -1;
+      if (live && !promo && (p & 7) == KING) {
+        const uint32_t cr = rights(sc.cr0, sc.ksq, w.pre);
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+          const int r = sc_cr(cr, us, side);
+          if (rsq < 0 && r >= 0 && (to == r || (!sc.c960 && to == back + (side == 0 ? 6 : 2)))) rsq = r;
+        }
+      }
+      return rsq;
+    };
+    int rsq = castle_rook(pc);
+    const bool castle = rsq >= 0;
+    const bool king_side = rsq > from;
+    const int kto = back + (king_side ? 6 : 2), rto = back + (king_side ? 5 : 3);
+    if (__ballot(castle)) {
+      w1 = castle ? kto : to;
+      w2 = castle ? rto : 64;
+      pc = resolve();
+    }
+    // en passant: the ep square before move j is the one move j - 1 left
+    const bool king = (pc & 7) == KING, pawn = (pc & 7) == PAWN;
+    const int new_ep = (!king && pawn && (from ^ to) == 16) ? (from + to) >> 1 : -1;
+    const int prev_ep = __shfl_up(new_ep, 1, 64);
+    const int ep = lane == 0 ? sc.ep : prev_ep;
+    const int cap = (!king && pawn && to == ep && ((from ^ to) & 7)) ? to + (us == WHITE ? -8 : 8) : 64;
+    const uint32_t placed = promo ? (uint32_t)make_piece_d(us, promo) : pc;
+    // this move's effect: clear c1, c2; write v1 at s1, v2 at s2 (64: none)
+    const int c1 = from, c2 = castle ? rsq : cap, s1 = castle ? kto : to, s2 = castle ? rto : 64;
+    const uint32_t v1 = castle ? pc : placed, v2 = (uint32_t)make_piece_d(us, ROOK);
+    const uint32_t pk = (uint32_t)c1 | (uint32_t)c2 << 7 | (uint32_t)s1 << 14 | (uint32_t)s2 << 21;
+    const uint32_t pv = v1 | v2 << 4;
+    mvw = live ? (castle ? ((uint32_t)from | ((uint32_t)rsq << 6) | (1u << 15))
+                         : ((uint32_t)from | ((uint32_t)to << 6) | ((uint32_t)promo << 12)))
+               : 0u;
+    scw[0] = live ? (uint32_t)new_ep : 0u;
+    replay::lds_fence();
+    uint32_t v = sqv;
+    for (uint32_t j = 0; j < kplay; ++j) {
+      const uint32_t a = replay::lane_value(pk, (int)j), b = replay::lane_value(pv, (int)j);
+      const uint32_t l = (uint32_t)lane;
+      v = (l == (a & 127u) || l == ((a >> 7) & 127u)) ? 0u : v;
+      v = l == ((a >> 14) & 127u) ? (b & 15u) : v;
+      v = l == ((a >> 21) & 127u) ? (b >> 4) : v;
+      reinterpret_cast<uint8_t*>(SNAP[j + 1])[lane] = (uint8_t)v;
+    }
+    sqv = v;
+    if (kplay) {
+      sc.ep = (int32_t)replay::lane_value((uint32_t)new_ep, (int)kplay - 1);
+      sc.stm ^= kplay & 1u;
+    }
+    replay::lds_fence();
+    return kplay;
+  }
   __device__ static uint32_t pack_move(const DMove& m) {
     return (uint32_t)m.from | ((uint32_t)m.to << 6) | ((uint32_t)m.promo << 12) | ((uint32_t)m.castle << 15);
   }

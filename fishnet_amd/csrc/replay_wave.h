@@ -283,6 +283,7 @@ template <class R>
 __device__ __forceinline__ uint32_t chain(typename R::Scalars& sc, uint32_t& sqv, uint32_t myc, uint32_t k,
                                           const typename R::Win& win, uint32_t (*SNAP)[16], int lane, uint32_t& mvw,
                                           uint32_t (&scw)[R::kVary]) {
+  if constexpr (R::kLaneChain) return R::lane_chain(sc, sqv, myc, k, win, SNAP, lane, mvw, scw);
   using Sc = typename R::Scalars;
   constexpr int kScw = sizeof(Sc) / 4;
   reinterpret_cast<uint8_t*>(SNAP[0])[lane] = (uint8_t)sqv;
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(64) void replay_wave_kernel(int variant, const char
   using Board = typename R::Board;
   using Sc = typename R::Scalars;
   static_assert(sizeof(Sc) % 4 == 0, "scalars as dwords");
-  __shared__ uint32_t SNAP[65][16];  // byte s of SNAP[j] = square s before the window's move j
+  __shared__ alignas(16) uint32_t SNAP[65][16];  // byte s of SNAP[j] = square s before the window's move j
   __shared__ uint32_t TK[kTokRing];  // pending token codes
   __shared__ char TXT[kTxt];         // move text from tbase on (' ' past the game's end)
   const uint32_t g = blockIdx.x;
@@ -460,7 +461,7 @@ struct PairLds {
   using Sc = typename R::Scalars;
   static constexpr int kScw = sizeof(Sc) / 4;
   static constexpr int kWinW = sizeof(typename R::Win) / 4 > 0 ? sizeof(typename R::Win) / 4 : 1;
-  uint32_t SNAP[2][65][16];
+  alignas(16) uint32_t SNAP[2][65][16];
   uint32_t TKW[2][64];          // the window's codes
   uint32_t MV[2][64];           // chain outputs per lane: move, scalars, Win
   uint32_t SCW[2][R::kVary][64];

@@ -49,6 +49,7 @@ struct VariantRules {
   // Along the chain the pockets, cr and ep change; stm alternates and the
   // variant word is fixed (the checking lanes derive those two).
   static constexpr int kVary = 6;
+  static constexpr bool kLaneChain = false;  // drops and explosions: the sequential chain (replay::chain)
   struct Win {};
   __device__ static Win window(const Scalars&, uint32_t, uint32_t, int) { return Win{}; }
   __device__ static void advance(Scalars&, const Win&, uint32_t) {}
