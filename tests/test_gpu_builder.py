@@ -131,3 +131,72 @@ def test_builder_feeds_evaluator(ev):
     a = ev.eval_groups(pos, off, N.GROUP_CHAIN)
     b = ev.eval_groups(hpos, hoff, N.GROUP_CHAIN)
     assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+# Move sequences whose later moves depend on what earlier moves of the same
+# replay window did (the lane-parallel chess chain, replay_wave.h /
+# ChessRules::lane_chain): castling in both notations followed by the king's
+# and the rook's next moves, queenside and Chess960 castling where the king
+# stays on its square, en passant taken and expired, promoted pieces moving
+# on, and moves from squares emptied earlier (illegal: the first failing ply).
+LANE_SEQS = [
+    (START, "e2e4 e7e5 g1f3 b8c6 f1c4 g8f6 e1g1 f8c5 f1e1 e8g8 g1h1 c6d4 e1e2 f8e8 h1g1"),
+    (START, "e2e4 e7e5 g1f3 b8c6 f1c4 g8f6 e1h1 f8c5 f1e1 e8h8 g1h1 c6d4 e1e2 f8e8 h1g1"),
+    (START, "d2d4 d7d5 b1c3 b8c6 c1f4 c8f5 d1d2 d8d7 e1c1 e8c8 d1e1 d8e8 c1b1 c8b8 e1d1"),
+    (START, "d2d4 d7d5 b1c3 b8c6 c1f4 c8f5 d1d2 d8d7 e1a1 e8a8 d1e1 d8e8 c1b1 c8b8 e1d1"),
+    (START, "e2e4 a7a6 e4e5 d7d5 e5d6 c7d6 d2d4 d6d5"),
+    (START, "e2e4 a7a6 e4e5 d7d5 a2a3 a6a5 e5d6"),
+    (START, "e2e4 e7e5 e2e3"),
+    (START, "e2e4 e7e5 g1f3 b8c6 f1c4 g8f6 e1g1 f8c5 h1g1"),
+    (START, "e2e4 e7e5 g1f3 b8c6 f1c4 g8f6 e1e2 f8c5 e2e1 d7d6 e1g1"),
+    ("8/P6k/8/8/8/8/6Kp/8 w - - 0 1", "a7a8q h2h1q a8a1 h1a1 g2f2 a1a2 f2e3 a2a8"),
+    ("8/P6k/8/8/8/8/6Kp/8 w - - 0 1", "a7a8n h2h1r a8b6 h1h2 g2g3 h2b2 b6d5 b2b3"),
+    ("r5kr/pppppppp/8/8/8/8/PPPPPPPP/R5KR w HAha - 0 1", "f2f4 f7f5 g1h1 g8h8 f1f3 f8f6 g1h1 g8h8 a1b1 a8b8"),
+    ("1rk1r3/pppppppp/8/8/8/8/PPPPPPPP/1RK1R3 w BEbe - 0 1", "f2f4 f7f5 c1e1 c8e8 f1f3 f8f6 g1h1 g8h8 b1c1 b8c8"),
+    ("1rk1r3/pppppppp/8/8/8/8/PPPPPPPP/1RK1R3 w BEbe - 0 1", "d2d4 d7d5 c1b1 c8b8 d1d3 d8d6 c1d1 c8d8 d1c1"),
+    ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "e1g1 e8c8 f1f8 d8f8 g1h1 c8b8 a1a8 b8a8"),
+    ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "a1a8 e8e7 a8h8 h8h1 e1h1"),
+    ("r3k2r/8/8/8/8/8/8/R3K2R w KQkq - 0 1", "h1h8 e8d7 e1g1"),
+]
+
+
+def _host_outcome(fen, moves):
+    """(positions, None) for a legal game, (None, first failing ply) else."""
+    mv = moves.split()
+    try:
+        return F.game_positions(fen, moves), None
+    except F.FnnueError:
+        k = 0
+        while True:
+            try:
+                F.game_positions(fen, " ".join(mv[:k + 1]))
+                k += 1
+            except F.FnnueError:
+                return None, k + 1
+
+
+def test_window_dependent_moves_match_host(ev):
+    """Every LANE_SEQS game, from its root and (standard start) after knight
+    shuffles of 28 / 56 / 60 plies that move its events across the 64-move
+    window boundary: legal games record for record equal to the host builder
+    (as one batch: the two-wave replay, and repeated past 1024 games: the
+    one-wave replay), illegal ones fail at the host's first failing ply."""
+    shuffle = "g1f3 g8f6 f3g1 f6g8"
+    games = []
+    for fen, moves in LANE_SEQS:
+        for r in ((0, 7, 14, 15) if fen == START else (0,)):
+            games.append((fen, " ".join([shuffle] * r + [moves]).strip()))
+    legal, illegal = [], []
+    for fen, moves in games:
+        pos, ply = _host_outcome(fen, moves)
+        (legal if ply is None else illegal).append((fen, moves, pos, ply))
+    assert len(legal) >= 20 and len(illegal) >= 20
+    for reps in (1, 1100 // len(legal) + 1):
+        batch = [(f, m) for f, m, _, _ in legal] * reps
+        pos, off = ev.build_batch(batch)
+        hpos, hoff = host_plies(batch)
+        assert np.array_equal(off, hoff) and np.array_equal(pos, hpos), reps
+    for fen, moves, _, ply in illegal:
+        with pytest.raises(F.FnnueError) as e:
+            ev.build_batch([(fen, moves)])
+        assert e.value.name == "FNNUE_E_MOVE" and f"ply {ply} of game 0" in str(e.value), (moves, str(e.value))
