@@ -436,6 +436,7 @@ struct fnnue_backend {
   int wait_event(hipEvent_t e, const char* what);
   bool streams_idle();
   void abandon_unanswered(Job& j);
+  void drain_streams();
   int prepare_moves(Job& j, int k);
   void layout(const Job& j, int k, Piece& P);
   int plan(Job& j, int k);
@@ -486,9 +487,26 @@ void fnnue_backend::abandon_unanswered(Job& j) {
       for (size_t i : W.pieces[pi].games) j.rc[i] = FNNUE_E_TIMEOUT;
     if (W.next < W.pieces.size())  // the move work rides in the net's last piece
       for (size_t i : W.roots) j.rc[i] = FNNUE_E_TIMEOUT;
-    for (size_t i : W.terminal) j.rc[i] = FNNUE_E_TIMEOUT;
   }
   broken = true;
+}
+
+// After an error other than the budget: the pinned images stay in use until
+// the device's copies are done, so the streams are drained before the call
+// returns — polled, and only until the call's deadline (a stuck device then
+// breaks the channel instead of hanging the caller).
+void fnnue_backend::drain_streams() {
+  for (uint32_t i = 0; !streams_idle(); ++i) {
+    if (expired()) {
+      broken = true;
+      return;
+    }
+    if (i < 512) {
+      for (int p = 0; p < 16; ++p) _mm_pause();
+    } else {
+      sched_yield();
+    }
+  }
 }
 
 // Move batches of one net, host side: the position after all moves (one per
@@ -1168,17 +1186,18 @@ void fnnue_backend::run(Job& j) {
     // is broken (later calls fail fast, fnnue_backend_free reclaims the
     // buffers once the streams have drained).
     abandon_unanswered(j);
+    // the answers that need no device (roots without a legal move, batches
+    // whose every position is skipped) are written: they are valid
+    fill_hostonly(j, all_skipped);
     j.ret = rc;
     j.err = g_err;
     return;
   }
   if (rc) {
-    for (int k = 0; k < kKinds; ++k) {  // the pinned images stay in use until the copies are done
-      if (!ctx[k]) continue;
-      (void)hipStreamSynchronize(ctx[k]->stream);
-    }
+    const std::string err = g_err;
+    drain_streams();
     j.ret = rc;
-    j.err = g_err;
+    j.err = err;
     return;
   }
   fill_hostonly(j, all_skipped);

@@ -584,16 +584,20 @@ def test_go_timeout_breaks_the_channel():
     on = {0: OracleNet(data)}
     bodies = [B.AcquireResponseBody(f"b{i}", GAMES[i % len(GAMES)]["position"], GAMES[i % len(GAMES)]["moves"])
               for i in range(16384)]
+    # answered without the device: their answers stand after a timeout
+    hostonly = [B.AcquireResponseBody("allskip", START, "e2e4", skip_positions=[0, 1]),
+                B.AcquireResponseBody("mated", START, FOOLS_MATE, work="move")]
     stub, actor = B.channel(F.Net.from_bytes(data), 0)
     try:
         warm = stub.go(bodies[:64])
         assert not any(isinstance(r, B.PositionFailed) for r in warm)
         with pytest.raises(F.FnnueError) as e:
-            stub.go(bodies, timeout_ms=1)
+            stub.go(hostonly[:1] + bodies + hostonly[1:], timeout_ms=1)
         assert e.value.name == "FNNUE_E_TIMEOUT", e.value
         assert stub.last_call_s < 1.0, stub.last_call_s
         rc = stub.last_batch_rc
         assert set(np.unique(rc).tolist()) <= {0, -11} and (rc == -11).sum() > 0
+        assert rc[0] == 0 and rc[-1] == 0, (rc[0], rc[-1])
         with pytest.raises(F.FnnueError) as e:
             stub.go(bodies[:4])
         assert e.value.name == "FNNUE_E_TIMEOUT" and stub.last_call_s < 0.05
