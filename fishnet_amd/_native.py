@@ -22,7 +22,8 @@ ERRORS = {
 SYNTH_LEB128, SYNTH_WRAP, SYNTH_FC1_PAD = 1, 2, 4
 GROUP_CHAIN, GROUP_STAR = 0, 1
 TIMING_OFF, TIMING_ALL, TIMING_FT = 0, 1, 2  # fnnue_ctx_set_timing
-FT_SLICED, FT_GATHER = 0, 1
+FT_SLICED, FT_GATHER, FT_AUTO = 0, 1, 2
+FT_GATHER_MAX = 16384  # FNNUE_FT_AUTO gathers chess positions calls up to this size
 PLAYOUT_FINAL, PLAYOUT_PLIES, PLAYOUT_CHILDREN = 0, 1, 2
 VARIANT_CHESS, VARIANT_CRAZYHOUSE, VARIANT_ATOMIC = 0, 1, 2
 POS_BYTES = 36

@@ -516,37 +516,47 @@ void fnnue_backend::drain_streams() {
 // beyond the variant's limits) — checked here, so that the device never
 // latches an error for move work (one bad batch no longer fails
 // the call).
+// The roots are replayed on the pool's threads (each root ~40-70 us of host
+// board work: its moves matched against the legal moves, then every child's
+// legal moves for its game-end flags), then merged in batch order.
 int fnnue_backend::prepare_moves(Job& j, int k) {
   NetWork& W = net[k];
   const bool chess = k == kVariantChess;
-  std::vector<fnnue_pos> kids;
-  std::vector<fnnue_vpos> vkids;
+  const size_t nr = W.roots.size();
+  std::vector<MoveRoot> R(nr);
+  std::vector<std::vector<fnnue_pos>> kids(chess ? nr : 0);
+  std::vector<std::vector<fnnue_vpos>> vkids(chess ? 0 : nr);
+  std::vector<int> rcs(nr, FNNUE_OK);
+  pool.run(nr, 1, [&](size_t lo, size_t hi) {
+    for (size_t t = lo; t < hi; ++t) {
+      const fnnue_acquired& a = j.batches[W.roots[t]];
+      int rc = chess ? chess_move_root(a, R[t], kids[t]) : variant_move_root(k, a, R[t], vkids[t]);
+      if (rc == FNNUE_OK && chess)
+        for (const fnnue_pos& p : kids[t]) rc = rc ? rc : (valid_host_pos(p) ? 0 : (int)FNNUE_E_POSITION);
+      if (rc == FNNUE_OK && !chess)
+        for (const fnnue_vpos& p : vkids[t]) rc = rc ? rc : (host_vpos_state(p, k) ? 0 : (int)FNNUE_E_POSITION);
+      rcs[t] = rc;
+    }
+  });
   std::vector<size_t> dev_roots;
-  for (size_t i : W.roots) {
-    MoveRoot R;
-    kids.clear();
-    vkids.clear();
-    int rc = chess ? chess_move_root(j.batches[i], R, kids) : variant_move_root(k, j.batches[i], R, vkids);
-    if (rc == FNNUE_OK) {
-      for (const fnnue_pos& p : kids) rc = rc ? rc : (valid_host_pos(p) ? 0 : (int)FNNUE_E_POSITION);
-      for (const fnnue_vpos& p : vkids) rc = rc ? rc : (host_vpos_state(p, k) ? 0 : (int)FNNUE_E_POSITION);
-    }
-    if (rc) {
-      j.rc[i] = rc;
+  for (size_t t = 0; t < nr; ++t) {
+    const size_t i = W.roots[t];
+    if (rcs[t]) {
+      j.rc[i] = rcs[t];
       continue;
     }
-    if (R.uci.empty()) {
+    if (R[t].uci.empty()) {
       W.terminal.push_back(i);
-      W.troots.push_back(std::move(R));
+      W.troots.push_back(std::move(R[t]));
       continue;
     }
-    const uint8_t* src = chess ? reinterpret_cast<const uint8_t*>(kids.data())
-                               : reinterpret_cast<const uint8_t*>(vkids.data());
-    const size_t cnt = chess ? kids.size() : vkids.size();
+    const uint8_t* src = chess ? reinterpret_cast<const uint8_t*>(kids[t].data())
+                               : reinterpret_cast<const uint8_t*>(vkids[t].data());
+    const size_t cnt = chess ? kids[t].size() : vkids[t].size();
     W.kid_first.push_back(W.nk);
     W.kids.insert(W.kids.end(), src, src + cnt * W.rec);
     W.nk += cnt;
-    W.mroots.push_back(std::move(R));
+    W.mroots.push_back(std::move(R[t]));
     dev_roots.push_back(i);
   }
   W.roots.swap(dev_roots);

@@ -127,7 +127,9 @@ int ctx_alloc(int device, uint32_t hd, fnnue_ctx** out, int variant) {
       hipMalloc(&P.psqt_part, (size_t)2 * chunk * sizeof(int32_t)) != hipSuccess)
     return fail(FNNUE_E_OOM, "device allocation (sliced plan)");
   if (const char* impl = std::getenv("FNNUE_FT_IMPL"))
-    c->ft_impl = std::strcmp(impl, "gather") == 0 ? FNNUE_FT_GATHER : FNNUE_FT_SLICED;
+    c->ft_impl = std::strcmp(impl, "gather") == 0   ? FNNUE_FT_GATHER
+                 : std::strcmp(impl, "sliced") == 0 ? FNNUE_FT_SLICED
+                                                    : FNNUE_FT_AUTO;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
   HIP_TRY(hipEventCreateWithFlags(&c->ws_event, hipEventDisableTiming), "hipEventCreate");
   c->ptrs = make_ptrs(c->image, hd, c->nfeat);
@@ -608,7 +610,8 @@ int fnnue_ctx_image(fnnue_ctx* ctx, const void** device_image, size_t* bytes) {
 void fnnue_ctx_free(fnnue_ctx* ctx) { ctx_destroy(ctx); }
 
 int fnnue_ctx_set_ft_impl(fnnue_ctx* ctx, int impl) {
-  if (!ctx || (impl != FNNUE_FT_SLICED && impl != FNNUE_FT_GATHER)) return fail(FNNUE_E_ARG, "bad ft impl");
+  if (!ctx || (impl != FNNUE_FT_SLICED && impl != FNNUE_FT_GATHER && impl != FNNUE_FT_AUTO))
+    return fail(FNNUE_E_ARG, "bad ft impl");
   ctx->ft_impl = impl;
   return FNNUE_OK;
 }
@@ -682,6 +685,9 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
   int rc = order_workspace(ctx, s);
   if (rc) return rc;
   WorkspaceUse use{ctx, s};
+  // FNNUE_FT_AUTO: a call of at most FNNUE_FT_GATHER_MAX positions gathers
+  // (the sliced path's plan and tile loads are a fixed cost it cannot amortise)
+  const bool gather = ctx->ft_impl == FNNUE_FT_GATHER || (ctx->ft_impl == FNNUE_FT_AUTO && n <= FNNUE_FT_GATHER_MAX);
   for (size_t b = 0; b < n; b += ctx->chunk) {
     const uint32_t m = (uint32_t)std::min<size_t>(ctx->chunk, n - b);
     std::array<hipEvent_t, 4>* ev = nullptr;
@@ -690,7 +696,7 @@ int fnnue_eval_positions_device(fnnue_ctx* ctx, const fnnue_pos* d_pos, size_t n
     if ((rc = record_event(ctx, ev, 0, s))) return rc;
     const uint32_t* perm = nullptr;
     const int32_t* psqt_part = nullptr;
-    if (ctx->ft_impl == FNNUE_FT_GATHER) {
+    if (gather) {
       if ((rc = record_event(ctx, ev, 1, s))) return rc;
       HIP_TRY(launch_ft_scratch(ctx->hd, d_pos + b, m, ctx->ptrs, ctx->x, d_psqt + b, ctx->bucket, ctx->err, s),
               "ft_scratch launch");
@@ -727,7 +733,7 @@ int eval_groups_device(fnnue_ctx* ctx, const void* d_pos, size_t pos_bytes, cons
   int rc = order_workspace(ctx, s);
   if (rc) return rc;
   WorkspaceUse use{ctx, s};
-  const bool sliced = ctx->ft_impl == FNNUE_FT_SLICED || ctx->variant != kVariantChess;
+  const bool sliced = ctx->ft_impl != FNNUE_FT_GATHER || ctx->variant != kVariantChess;
   if (sliced && ((rc = ensure_seg(ctx)) || (rc = ensure_span(ctx, npos)))) return rc;
   if (sliced && npos <= seg_small_plan_max()) {
     // a small call (a game or a few): spans, the offset check and the whole
@@ -790,7 +796,7 @@ int eval_groups_dual_device(fnnue_ctx* a, fnnue_ctx* b, const fnnue_pos* d_pos, 
   if (a->variant != kVariantChess || b->variant != kVariantChess)
     return fail(FNNUE_E_ARCH, "dual evaluation: two chess (HalfKAv2_hm) nets");
   if (a->device != b->device) return fail(FNNUE_E_ARG, "the two contexts must be on one device");
-  if (a->ft_impl != FNNUE_FT_SLICED || b->ft_impl != FNNUE_FT_SLICED)
+  if (a->ft_impl == FNNUE_FT_GATHER || b->ft_impl == FNNUE_FT_GATHER)
     return fail(FNNUE_E_ARG, "dual evaluation runs on the sliced feature transformer");
   if (mode != FNNUE_GROUP_CHAIN && mode != FNNUE_GROUP_STAR) return fail(FNNUE_E_ARG, "bad group mode");
   if (ngroups == 0) return npos == 0 ? FNNUE_OK : fail(FNNUE_E_ARG, "positions without groups");

@@ -40,7 +40,7 @@ struct fnnue_ctx {
   char* d_btext = nullptr;     // fnnue_build_batch input staging (text, then FEN / move offsets), grow-only
   size_t btext_cap = 0;
   fnnue::BuilderScratch bscratch;  // the device batch builder's temporaries, grow-only
-  int ft_impl = FNNUE_FT_SLICED;
+  int ft_impl = FNNUE_FT_AUTO;
   int32_t acc_bound = 0;       // accumulator_bound of the net (SWAR rows allowed below 2^15)
   fnnue::SlicedPlan plan{};
   fnnue::SegPlan seg{};                // incremental sliced path for groups (allocated on first use)

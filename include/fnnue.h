@@ -379,16 +379,23 @@ int fnnue_random_game(uint64_t seed, const char *fen, uint32_t plies, char *move
  * layout matches the kernels' assumption. */
 int fnnue_selftest_mfma(int device);
 /* Feature-transformer implementation for fnnue_eval_positions*:
- *  FNNUE_FT_SLICED (default): LDS-stationary weight tiles, positions planned
- *    and sorted on the device; for fnnue_eval_groups*, the
- *    incremental updates run on the same tiles (segments of positions that
- *    share the perspective's king square).
+ *  FNNUE_FT_SLICED: LDS-stationary weight tiles, positions planned and sorted
+ *    on the device; for fnnue_eval_groups*, the incremental
+ *    updates run on the same tiles (segments of positions that share the
+ *    perspective's king square).
  *  FNNUE_FT_GATHER: one wave per position (groups: per group) gathering rows
  *    from L2/HBM.
- * Both are bit-identical; the environment variable FNNUE_FT_IMPL=gather|sliced
- * sets the default for new contexts. */
+ *  FNNUE_FT_AUTO (default): chess positions calls of at most
+ *    FNNUE_FT_GATHER_MAX positions gather (the sliced plan and its tile loads
+ *    are a fixed ~60-80 us that a small call does not amortise: move work's
+ *    children, a few games' positions), larger ones and every grouped call
+ *    run sliced.
+ * All are bit-identical; the environment variable FNNUE_FT_IMPL=
+ * gather|sliced|auto sets the default for new contexts. */
 #define FNNUE_FT_SLICED 0
 #define FNNUE_FT_GATHER 1
+#define FNNUE_FT_AUTO 2
+#define FNNUE_FT_GATHER_MAX 16384
 int fnnue_ctx_set_ft_impl(fnnue_ctx *ctx, int impl);
 /* SWAR row sums in the sliced feature transformer: pairs of int16 columns
  * summed as 32-bit words.  Exact whenever no reachable

@@ -68,15 +68,17 @@ def test_other_nets(ev_cache, seed, hd, flags):
     assert_same(ev, on, F.random_playouts(seed + 100, 3000, threads=8))
 
 
-@pytest.mark.parametrize("impl", [N.FT_SLICED, N.FT_GATHER])
-@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 65, 1000, 2049, 4097])
+@pytest.mark.parametrize("impl", [N.FT_SLICED, N.FT_GATHER, N.FT_AUTO])
+@pytest.mark.parametrize("n", [1, 2, 15, 16, 17, 63, 65, 1000, 2049, 4097, N.FT_GATHER_MAX, N.FT_GATHER_MAX + 1])
 def test_ragged_batch_sizes(ev_cache, n, impl):
+    """Every size through each feature-transformer choice (FNNUE_FT_AUTO, the
+    default, gathers up to FNNUE_FT_GATHER_MAX positions and runs sliced above)."""
     ev, on = ev_cache()
     ev.set_ft_impl(impl)
     try:
         assert_same(ev, on, F.random_playouts(50 + n, n, threads=4))
     finally:
-        ev.set_ft_impl(N.FT_SLICED)
+        ev.set_ft_impl(N.FT_AUTO)
 
 
 @pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (3, 1024, N.SYNTH_WRAP), (6, 2048, 0),
@@ -88,7 +90,7 @@ def test_ft_impls_agree(ev_cache, seed, hd, flags):
     a = ev.eval_positions(pos)
     ev.set_ft_impl(N.FT_GATHER)
     b = ev.eval_positions(pos)
-    ev.set_ft_impl(N.FT_SLICED)
+    ev.set_ft_impl(N.FT_AUTO)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     idx = np.arange(0, len(pos), 7)
     ops, opo, rc = on.eval_packed(pos[idx], threads=8)
@@ -130,7 +132,7 @@ def test_gather_groups_across_chunks(ev_cache):
     for impl in (N.FT_SLICED, N.FT_GATHER):
         ev.set_ft_impl(impl)
         res.append(ev.eval_groups(gpos, off, N.GROUP_CHAIN))
-    ev.set_ft_impl(N.FT_SLICED)
+    ev.set_ft_impl(N.FT_AUTO)
     assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
     idx = np.r_[0:1000, chunk - 2000:chunk + 2000, len(gpos) - 1000:len(gpos)]
     ops, opo, rc = on.eval_packed(gpos[idx], threads=8)
@@ -334,7 +336,7 @@ def test_group_impls_agree(ev_cache, seed, hd, flags):
         for impl in (N.FT_SLICED, N.FT_GATHER):
             ev.set_ft_impl(impl)
             res.append(ev.eval_groups(pos, off, mode))
-        ev.set_ft_impl(N.FT_SLICED)
+        ev.set_ft_impl(N.FT_AUTO)
         ops, opo, rc = on.eval_packed(pos, threads=8)
         for ps, po in res:
             assert np.array_equal(ps, ops) and np.array_equal(po, opo)
@@ -598,7 +600,7 @@ def test_device_groups_above_one_workspace(ev_cache):
                     ev.check()
                 assert e.value.name == "FNNUE_E_ARG"
             finally:
-                ev.set_ft_impl(N.FT_SLICED)
+                ev.set_ft_impl(N.FT_AUTO)
 
 
 @pytest.mark.parametrize("seed,hd,flags", [(1, 1024, 0), (7, 128, 0), (6, 2048, 0), (8, 1536, N.SYNTH_LEB128)])
