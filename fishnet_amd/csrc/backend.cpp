@@ -232,19 +232,19 @@ int chess_move_root(const fnnue_acquired& a, MoveRoot& R, std::vector<fnnue_pos>
     }
     if (!*p) break;
   }
-  auto fin_of = [](const Board& x, const std::vector<Move>& ms) {
-    return (uint8_t)((ms.empty() ? kFinalNoMoves : 0) | (x.in_check() ? kFinalCheck : 0));
+  auto fin_of = [](const Board& x, bool any) {
+    return (uint8_t)((any ? 0 : kFinalNoMoves) | (x.in_check() ? kFinalCheck : 0));
   };
-  std::vector<Move> ms, km;
+  std::vector<Move> ms;
   b.legal_moves(ms);
-  R.fin = fin_of(b, ms);
+  R.fin = fin_of(b, !ms.empty());
+  kids.reserve(ms.size());
   for (const Move& m : ms) {
     Board k = b;
     k.do_move(m);
-    k.legal_moves(km);
     kids.push_back(k.pack());
     R.uci.push_back(b.uci(m, b.chess960));
-    R.kid_fin.push_back(fin_of(k, km));
+    R.kid_fin.push_back(fin_of(k, k.has_legal_move()));
   }
   return FNNUE_OK;
 }

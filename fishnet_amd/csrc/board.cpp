@@ -347,13 +347,29 @@ bool board_from_fen(const char* fen, Board& b, std::string* err) {
   return true;
 }
 
+// The first legal move that prints as the token (either castling notation
+// outside Chess960).  Every move prints its own from-square first, so only
+// the pseudo-legal moves from the token's first square are checked for
+// legality and printed: the same first match as scanning every legal move.
 bool parse_uci(const Board& b, const char* uci, Move& out) {
-  std::vector<Move> moves;
-  b.legal_moves(moves);
   const std::string u(uci ? uci : "");
-  for (const Move& m : moves) {
+  if (u.size() < 4 || u[0] < 'a' || u[0] > 'h' || u[1] < '1' || u[1] > '8') return false;
+  const int from = (u[1] - '1') * 8 + (u[0] - 'a');
+  Move buf[256];
+  const int nm = b.pseudo_moves(buf);
+  for (int i = 0; i < nm; ++i) {
+    const Move& m = buf[i];
+    if (m.from != from || !b.is_legal(m)) continue;
     if (b.uci(m, true) == u || (!b.chess960 && b.uci(m, false) == u)) { out = m; return true; }
   }
+  return false;
+}
+
+bool Board::has_legal_move() const {
+  Move buf[256];
+  const int nm = pseudo_moves(buf);
+  for (int i = 0; i < nm; ++i)
+    if (is_legal(buf[i])) return true;
   return false;
 }
 

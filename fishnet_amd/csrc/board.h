@@ -49,6 +49,7 @@ struct Board {
   bool is_legal(const Move& m) const;
   // All legal moves.
   void legal_moves(std::vector<Move>& out) const;
+  bool has_legal_move() const;  // legal_moves non-empty, stopping at the first
   // Uniformly random legal move by rejection sampling over the pseudo-legal
   // list; false if there is none.  rng is a splitmix64 state.
   bool random_legal_move(uint64_t& rng, Move& out) const;
