@@ -1067,11 +1067,56 @@ def run(args) -> dict | None:
     return out if rank == 0 else None
 
 
+def move_work_line(args) -> dict:
+    """The engine actor's move work (Work::Move, [ref] src/api.rs:160-165: the
+    position after all moves, a one-ply search over its legal children) at 1
+    and 8 move batches per go(): median latency over repeated calls; spot
+    check: each answer's best child evaluated by the oracle (its psqt /
+    positional negated) and its legal-children count."""
+    import fishnet_amd as F
+    from fishnet_amd import backend as B
+    from oracle.oracle import OracleNet  # spot check only (test infrastructure)
+    net = F.synthesize_net(args.seed, args.hd, 0)
+    stub, actor = B.channel(F.Net.from_bytes(net), 0)
+    on = OracleNet(net)
+    rows, checked, bad = [], 0, 0
+    try:
+        pool = [b for b in lichess_batches(F, args.seed + 17, 64) if b.variant in ("standard", "chess960")]
+        for nb in (1, 8):
+            bodies = [B.AcquireResponseBody(f"m{i}", b.position, b.moves, work="move", variant=b.variant)
+                      for i, b in enumerate(pool[:nb])]
+            for _ in range(10):
+                res = stub.go(bodies)
+            ts, t_end = [], time.perf_counter() + 0.3
+            while time.perf_counter() < t_end or len(ts) < 20:
+                t = time.perf_counter()
+                res = stub.go(bodies)
+                ts.append((time.perf_counter() - t) * 1e3)
+            for b, r in zip(bodies, res):
+                (r,) = r
+                _, goff = F.game_children(b.position, b.moves)  # the last group: the root and its children
+                checked += 1
+                ok = r.nodes == int(goff[-1]) - int(goff[-2]) - 1
+                if ok and r.best_move and r.score.kind == "cp":
+                    child = F.game_positions(b.position, b.moves + " " + r.best_move)[-1:]
+                    ps, po, rc = on.eval_packed(child)
+                    ok = rc == 0 and r.psqt == -int(ps[0]) and r.positional == -int(po[0])
+                bad += 0 if ok else 1
+            rows.append({"move_batches_per_go": nb, "children": int(sum(r[0].nodes for r in res)),
+                         "calls": len(ts), "ms_per_go_median": round(float(np.median(ts)), 4)})
+    finally:
+        actor.close()
+    return {"workload": "fnnue_backend_go over move batches (the position after 40-160 random legal moves, "
+                        "standard and Chess960; best child by a one-ply search over the legal children)",
+            "per_batches": rows, "parity_spot_check": {"checked": checked, "mismatches": bad}}
+
+
 def extra_lines(args) -> dict:
     """The default run's extra workloads, measured after
     the headline and outside its timed steps: BASELINE config 3 with the big +
-    small net through the dual call (20 steps), and the engine actor at 1 / 64
-    / 1024 acquired batches per go(); each with its own oracle spot check."""
+    small net through the dual call (20 steps), the engine actor at 1 / 64 /
+    1024 acquired batches per go(), and its move work at 1 / 8 move batches;
+    each with its own oracle spot check."""
     extra = {}
     t0 = time.time()
     a3 = argparse.Namespace(**vars(args))
@@ -1100,6 +1145,7 @@ def extra_lines(args) -> dict:
         "roofline": o.get("roofline"),
         "cpu_baseline": {k: o["cpu_baseline"][k] for k in ("value", "unit", "cores", "kind")}
         if o.get("cpu_baseline") else None}
+    extra["move_work"] = move_work_line(args)
     extra["seconds"] = round(time.time() - t0, 1)
     return extra
 
