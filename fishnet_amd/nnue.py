@@ -364,7 +364,9 @@ class Evaluator:
         return nodes.value
 
     def set_ft_impl(self, impl: int) -> None:
-        """FT_SLICED (default, LDS-stationary tiles) or FT_GATHER (per-position row gather)."""
+        """FT_AUTO (default: gather for chess position calls of at most FT_GATHER_MAX positions,
+        sliced otherwise and for every grouped call), FT_SLICED (LDS-stationary tiles) or
+        FT_GATHER (per-position / per-group row gather)."""
         N.check(N.lib.fnnue_ctx_set_ft_impl(self._h, impl))
 
     def swar(self) -> tuple[bool, int]:
